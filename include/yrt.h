@@ -1,0 +1,131 @@
+/* yrt.h -- C-ABI of the MI355X-native renderer for the yocto_raytracing hot path.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes, no
+ * exceptions and no torch types across the boundary. Every entry point names the
+ * reference interface it replaces (reference = sebcossu/yocto_raytracing, src/).
+ *
+ * Typical use, mirroring main() in src/raytrace.cpp:256-287:
+ *     yrt_host_scene* hs;  yrt_scene_load("scene.obj", &hs);       // load_scene
+ *     yrt_host_scene_build_bvh(hs, 0);                             // build_bvh(scn, false)
+ *     yrt_scene* ds;  yrt_scene_upload(hs, 0, &ds);                // (new) copy to HBM
+ *     yrt_render_params p;  yrt_render_params_default(&p);  p.resolution = 720; p.samples = 3;
+ *     int w, h;  yrt_image_size(ds, &p, &w, &h);
+ *     yrt_render(ds, &p, host_rgba_w_h_4, YRT_MEM_HOST, NULL);     // raytrace()
+ *     yrt_save_image("out.png", host_rgba_w_h_4, w, h);            // save_hdr_or_ldr
+ */
+#ifndef YRT_H
+#define YRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YRT_ABI_VERSION 1
+
+/* status codes (the reference has none: it exit(1)s in the loader, scene.cpp:119-122) */
+enum {
+    YRT_OK = 0,
+    YRT_ERR_INVALID_ARG = 1,
+    YRT_ERR_IO = 2,          /* file missing / unreadable / malformed */
+    YRT_ERR_UNSUPPORTED = 3, /* input the kernels do not handle (mixed shapes, hdr textures, deep BVH) */
+    YRT_ERR_HIP = 4,         /* HIP runtime error (message via yrt_last_error) */
+    YRT_ERR_NO_DEVICE = 5,
+    YRT_ERR_OOM = 6,
+    YRT_ERR_INTERNAL = 7
+};
+
+typedef struct yrt_host_scene yrt_host_scene; /* host scene + BVH (scene*, scene.h:136-155) */
+typedef struct yrt_scene yrt_scene;           /* scene resident in one GPU's HBM */
+
+/* memory location of a caller buffer */
+enum { YRT_MEM_HOST = 0, YRT_MEM_DEVICE = 1 };
+
+typedef struct yrt_render_params {
+    float ambient[3];  /* raytrace(..., amb, ...): main() passes {a,a,a}, a = -a (0.1) */
+    int resolution;    /* vertical resolution -r (raytrace.cpp:216) */
+    int width;         /* 0: round(camera.aspect * resolution) as the reference; >0: explicit */
+    int samples;       /* -s: samples PER AXIS, s*s per pixel (raytrace.cpp:232-234) */
+    int max_depth;     /* trace_first calls per camera sample; reference: unbounded. 0 -> 16 */
+    int camera;        /* camera index; reference: cameras.front() == 0 */
+    int x0, y0;        /* window origin in image pixels */
+    int tile_w, tile_h;/* window size; 0 -> to the image edge */
+    int band;          /* row interleave for multi-GPU sharding: rows are taken in bands of */
+    int band_stride;   /*   `band` rows; local band b is image band b*band_stride+band_offset */
+    int band_offset;   /*   (band=1,stride=1,offset=0: contiguous rows) */
+    int out_stride;    /* output row stride in pixels; 0 -> tile_w */
+    int count_work;    /* 1: also count box/instance/primitive tests (slower; for roofline bytes) */
+} yrt_render_params;
+
+/* counters accumulated by the last yrt_render / yrt_trace_* on a scene handle */
+typedef struct yrt_stats {
+    unsigned long long rays;            /* intersect_first + intersect_any calls */
+    unsigned long long camera_samples;  /* eval_camera calls */
+    unsigned long long depth_truncated; /* paths cut by max_depth (0 = parity-neutral) */
+    unsigned long long stack_overflow;
+    unsigned long long box_tests;       /* count_work only */
+    unsigned long long instance_entries;
+    unsigned long long prim_tests;
+    unsigned long long shaded_hits;
+    unsigned long long texture_lookups;
+} yrt_stats;
+
+/* ---- library ---- */
+int yrt_abi_version(void);
+const char* yrt_status_string(int status);
+/* message of the last error on this thread (empty string if none) */
+const char* yrt_last_error(void);
+int yrt_device_count(int* count);
+
+/* ---- host scene: loader, serialisation, BVH ---- */
+/* load_scene (src/scene.cpp:113-225): Yocto OBJ (.obj) or the .yrtscene interchange file */
+int yrt_scene_load(const char* path, yrt_host_scene** out);
+/* serialise the shading-relevant arrays (.yrtscene, gzip) */
+int yrt_scene_save(const yrt_host_scene* hs, const char* path);
+/* build_bvh(scene*, bool equal_num) (src/scene.cpp:554-565, decl scene.h:238) */
+int yrt_host_scene_build_bvh(yrt_host_scene* hs, int equal_num);
+/* dump the BVHs (.yrtbvh) byte-compatible with the reference's bvh_node (scene.h:9-15) */
+int yrt_host_scene_save_bvh(const yrt_host_scene* hs, const char* path);
+/* counts: [cameras, textures, materials, shapes, instances, lights, bvh nodes(instance
+ * level), bvh depth(instance level), max shape bvh depth, triangles, lines, points] */
+int yrt_host_scene_info(const yrt_host_scene* hs, long long* info12);
+/* image size raytrace() would produce: W = round(aspect*res), H = res (raytrace.cpp:215-216) */
+int yrt_host_image_size(const yrt_host_scene* hs, int camera, int resolution, int* w, int* h);
+void yrt_host_scene_free(yrt_host_scene* hs);
+
+/* ---- device scene ---- */
+/* flatten to the HBM layout and upload to `device` (needs a built BVH) */
+int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out);
+size_t yrt_scene_device_bytes(const yrt_scene* ds);
+void yrt_scene_free(yrt_scene* ds);
+
+/* ---- the hot path ---- */
+void yrt_render_params_default(yrt_render_params* p);
+int yrt_image_size(const yrt_scene* ds, const yrt_render_params* p, int* w, int* h);
+/* raytrace() (src/raytrace.cpp:213-254). out: RGBA f32, row-major pixels[j*W+i]
+ * (image4f, image.h:8-17) restricted to the params window/bands; `mem` says whether
+ * `out` is a host or device pointer; `stream` is a hipStream_t (NULL = default).
+ * A host `out` makes the call synchronous; a device `out` is stream-ordered. */
+int yrt_render(yrt_scene* ds, const yrt_render_params* p, float* out, int mem, void* stream);
+/* batch intersect_first (src/scene.cpp:483-488). rays: n x {o.xyz, d.xyz, tmin, tmax}.
+ * Outputs per ray: hit (0/1), instance index (-1 on miss), element index ei (-1 on miss),
+ * ew[4] barycentrics, dist. All pointers in `mem` space. */
+int yrt_trace_first(yrt_scene* ds, const float* rays, int n, unsigned char* hit, int* inst, int* ei,
+                    float* ew, float* dist, int mem, void* stream);
+/* batch intersect_any (src/scene.cpp:489-493) */
+int yrt_trace_any(yrt_scene* ds, const float* rays, int n, unsigned char* hit, int mem, void* stream);
+/* counters of the last render/trace call on this handle (synchronises the stream) */
+int yrt_last_stats(yrt_scene* ds, yrt_stats* stats);
+
+/* ---- image output ---- */
+/* tonemap (src/image.cpp:55-77, exposure 0, srgb) of n RGBA f32 pixels into RGBA8 */
+int yrt_tonemap(const float* rgba, int n, unsigned char* out, int mem, void* stream);
+/* save_hdr_or_ldr (src/image.cpp:81-88): .hdr -> RGBE, else PNG of the tonemap */
+int yrt_save_image(const char* path, const float* rgba, int w, int h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YRT_H */

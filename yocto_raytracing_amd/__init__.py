@@ -1,0 +1,233 @@
+"""yocto_raytracing_amd -- MI355X-native renderer for the yocto_raytracing hot path.
+
+Python mirror of the reference's host interface (names, argument meaning and
+error behaviour of src/scene.h and src/raytrace.cpp), over the C-ABI of
+include/yrt.h implemented by libyrt.so (C++ host code + gfx950 HIP kernels):
+
+    scn = load_scene("in/basic_pointlight/basic_pointlight.obj")   # scene.cpp:113
+    build_bvh(scn, False)                                          # scene.cpp:554
+    img = raytrace(scn, (0.1, 0.1, 0.1), 720, 1)                   # raytrace.cpp:213
+    save_hdr_or_ldr("out.png", img)                                # image.cpp:81
+
+`img` is the reference's image4f: float32 RGBA, shape (H, W, 4), pixels[j][i].
+There is no CPU fallback: without a GPU the render calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from ._native import RenderParams, Stats, YrtError, check
+
+__all__ = [
+    "Scene", "DeviceScene", "load_scene", "build_bvh", "raytrace", "intersect_first",
+    "intersect_any", "tonemap", "save_hdr_or_ldr", "render_params", "device_count", "YrtError",
+]
+
+INFO_FIELDS = ("cameras", "textures", "materials", "shapes", "instances", "lights",
+               "bvh_nodes", "bvh_depth", "shape_bvh_depth", "triangles", "lines", "points")
+
+
+class Scene:
+    """Host scene (the reference's `scene*`), owned by libyrt."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+        self._device_scenes = {}
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        try:
+            for ds in self._device_scenes.values():
+                ds.close()
+            if self._h:
+                N.lib.yrt_host_scene_free(self._h)
+                self._h = C.c_void_p()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        buf = (C.c_longlong * 12)()
+        check(N.lib.yrt_host_scene_info(self._h, buf), "yrt_host_scene_info")
+        return dict(zip(INFO_FIELDS, list(buf)))
+
+    def image_size(self, resolution: int, camera: int = 0):
+        w, h = C.c_int(), C.c_int()
+        check(N.lib.yrt_host_image_size(self._h, camera, resolution, C.byref(w), C.byref(h)),
+              "yrt_host_image_size")
+        return w.value, h.value
+
+    def save(self, path: str) -> None:
+        check(N.lib.yrt_scene_save(self._h, str(path).encode()), "yrt_scene_save")
+
+    def save_bvh(self, path: str) -> None:
+        check(N.lib.yrt_host_scene_save_bvh(self._h, str(path).encode()), "yrt_host_scene_save_bvh")
+
+    def upload(self, device: int = 0) -> "DeviceScene":
+        if device not in self._device_scenes:
+            self._device_scenes[device] = DeviceScene(self, device)
+        return self._device_scenes[device]
+
+
+class DeviceScene:
+    """A scene resident in one GPU's HBM (yrt_scene*)."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        h = C.c_void_p()
+        check(N.lib.yrt_scene_upload(scene.handle, device, C.byref(h)), "yrt_scene_upload")
+        self._h = h
+        self.device = device
+        self.host = scene
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            N.lib.yrt_scene_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_bytes(self) -> int:
+        return int(N.lib.yrt_scene_device_bytes(self._h))
+
+    def image_size(self, params: RenderParams):
+        w, h = C.c_int(), C.c_int()
+        check(N.lib.yrt_image_size(self._h, C.byref(params), C.byref(w), C.byref(h)), "yrt_image_size")
+        return w.value, h.value
+
+    def render_into(self, params: RenderParams, out_ptr: int, device_memory: bool = True,
+                    stream: Optional[int] = None) -> None:
+        """Launch raytrace() into a caller buffer (device pointer by default), stream ordered."""
+        mem = N.YRT_MEM_DEVICE if device_memory else N.YRT_MEM_HOST
+        check(N.lib.yrt_render(self._h, C.byref(params), C.c_void_p(out_ptr), mem,
+                               C.c_void_p(stream or 0)), "yrt_render")
+
+    def last_stats(self) -> dict:
+        s = Stats()
+        check(N.lib.yrt_last_stats(self._h, C.byref(s)), "yrt_last_stats")
+        return {name: int(getattr(s, name)) for name, _ in Stats._fields_}
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    N.lib.yrt_device_count(C.byref(n))
+    return n.value
+
+
+def load_scene(filename: str) -> Scene:
+    """load_scene (src/scene.cpp:113): Yocto OBJ or .yrtscene. Raises on failure
+    (the reference prints "could not load scene" and exits)."""
+    h = C.c_void_p()
+    check(N.lib.yrt_scene_load(str(filename).encode(), C.byref(h)), f"load_scene({filename})")
+    return Scene(h.value)
+
+
+def build_bvh(scn: Scene, equal_num: bool = False) -> None:
+    """build_bvh (src/scene.cpp:554): per-shape BVHs, then the instance BVH."""
+    check(N.lib.yrt_host_scene_build_bvh(scn.handle, 1 if equal_num else 0), "build_bvh")
+
+
+def render_params(amb=(0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1, *,
+                  width: int = 0, max_depth: int = 16, camera: int = 0, window=None,
+                  band=(1, 1, 0), count_work: bool = False) -> RenderParams:
+    p = RenderParams()
+    N.lib.yrt_render_params_default(C.byref(p))
+    if np.isscalar(amb):
+        amb = (amb, amb, amb)
+    for k in range(3):
+        p.ambient[k] = float(amb[k])
+    p.resolution, p.samples, p.width = int(resolution), int(samples), int(width)
+    p.max_depth, p.camera = int(max_depth), int(camera)
+    if window is not None:
+        p.x0, p.y0, p.tile_w, p.tile_h = (int(v) for v in window)
+    p.band, p.band_stride, p.band_offset = (int(v) for v in band)
+    p.count_work = 1 if count_work else 0
+    return p
+
+
+def _device_scene(scn, device: int = 0) -> DeviceScene:
+    if isinstance(scn, DeviceScene):
+        return scn
+    return scn.upload(device)
+
+
+def raytrace(scn, amb: Sequence[float] = (0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1,
+             *, width: int = 0, max_depth: int = 16, camera: int = 0, window=None,
+             count_work: bool = False, return_stats: bool = False):
+    """raytrace (src/raytrace.cpp:213): RGBA float32 image (H, W, 4), row-major.
+
+    `samples` is per axis (s*s samples per pixel), `resolution` the vertical size.
+    `window` = (x0, y0, w, h) renders a sub-rectangle only."""
+    ds = _device_scene(scn)
+    p = render_params(amb, resolution, samples, width=width, max_depth=max_depth, camera=camera,
+                      window=window, count_work=count_work)
+    W, H = ds.image_size(p)
+    if window is None:
+        w, h = W, H
+    else:
+        w, h = window[2] or W - window[0], window[3] or H - window[1]
+    img = np.zeros((h, w, 4), np.float32)
+    ds.render_into(p, img.ctypes.data, device_memory=False)
+    if return_stats:
+        return img, ds.last_stats()
+    return img
+
+
+def _rays_array(rays) -> np.ndarray:
+    r = np.ascontiguousarray(rays, dtype=np.float32)
+    if r.ndim != 2 or r.shape[1] != 8:
+        raise ValueError("rays must be (n, 8): o.xyz, d.xyz, tmin, tmax")
+    return r
+
+
+def intersect_first(scn, rays) -> dict:
+    """Batch intersect_first (src/scene.cpp:483): per ray hit, instance, ei, ew[4], dist."""
+    ds = _device_scene(scn)
+    r = _rays_array(rays)
+    n = r.shape[0]
+    out = {"hit": np.zeros(n, np.uint8), "inst": np.zeros(n, np.int32), "ei": np.zeros(n, np.int32),
+           "ew": np.zeros((n, 4), np.float32), "dist": np.zeros(n, np.float32)}
+    check(N.lib.yrt_trace_first(ds.handle, r.ctypes.data, n, out["hit"].ctypes.data,
+                                out["inst"].ctypes.data, out["ei"].ctypes.data, out["ew"].ctypes.data,
+                                out["dist"].ctypes.data, N.YRT_MEM_HOST, None), "intersect_first")
+    out["hit"] = out["hit"].astype(bool)
+    return out
+
+
+def intersect_any(scn, rays) -> np.ndarray:
+    """Batch intersect_any (src/scene.cpp:489): occluded flag per ray."""
+    ds = _device_scene(scn)
+    r = _rays_array(rays)
+    hit = np.zeros(r.shape[0], np.uint8)
+    check(N.lib.yrt_trace_any(ds.handle, r.ctypes.data, r.shape[0], hit.ctypes.data, N.YRT_MEM_HOST,
+                              None), "intersect_any")
+    return hit.astype(bool)
+
+
+def tonemap(img: np.ndarray) -> np.ndarray:
+    """tonemap (src/image.cpp:55, exposure 0, srgb): RGBA8 of the same shape."""
+    a = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros(a.shape, np.uint8)
+    check(N.lib.yrt_tonemap(a.ctypes.data, a.size // 4, out.ctypes.data, N.YRT_MEM_HOST, None), "tonemap")
+    return out
+
+
+def save_hdr_or_ldr(filename: str, img: np.ndarray) -> None:
+    """save_hdr_or_ldr (src/image.cpp:81): .hdr -> RGBE, otherwise tonemapped PNG."""
+    a = np.ascontiguousarray(img, dtype=np.float32)
+    check(N.lib.yrt_save_image(str(filename).encode(), a.ctypes.data, a.shape[1], a.shape[0]),
+          "save_hdr_or_ldr")

@@ -1,0 +1,95 @@
+"""ctypes binding of include/yrt.h (libyrt.so, built in-tree).
+
+The library is the product: nothing here falls back to Python or to the CPU. If
+libyrt.so is missing or fails to load, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("YRT_LIB", _PKG / "libyrt.so"))
+
+if not LIB_PATH.exists():
+    raise ImportError(
+        f"{LIB_PATH} not found: build it with `python -m yocto_raytracing_amd.build` "
+        "(or __graft_entry__.build()); there is no fallback path")
+
+lib = C.CDLL(str(LIB_PATH))
+
+YRT_OK = 0
+YRT_MEM_HOST = 0
+YRT_MEM_DEVICE = 1
+
+
+class RenderParams(C.Structure):
+    _fields_ = [
+        ("ambient", C.c_float * 3),
+        ("resolution", C.c_int),
+        ("width", C.c_int),
+        ("samples", C.c_int),
+        ("max_depth", C.c_int),
+        ("camera", C.c_int),
+        ("x0", C.c_int),
+        ("y0", C.c_int),
+        ("tile_w", C.c_int),
+        ("tile_h", C.c_int),
+        ("band", C.c_int),
+        ("band_stride", C.c_int),
+        ("band_offset", C.c_int),
+        ("out_stride", C.c_int),
+        ("count_work", C.c_int),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_ulonglong) for n in (
+        "rays", "camera_samples", "depth_truncated", "stack_overflow", "box_tests",
+        "instance_entries", "prim_tests", "shaded_hits", "texture_lookups")]
+
+
+_vp = C.c_void_p
+_sig = {
+    "yrt_abi_version": (C.c_int, []),
+    "yrt_status_string": (C.c_char_p, [C.c_int]),
+    "yrt_last_error": (C.c_char_p, []),
+    "yrt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "yrt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
+    "yrt_scene_save": (C.c_int, [_vp, C.c_char_p]),
+    "yrt_host_scene_build_bvh": (C.c_int, [_vp, C.c_int]),
+    "yrt_host_scene_save_bvh": (C.c_int, [_vp, C.c_char_p]),
+    "yrt_host_scene_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
+    "yrt_host_image_size": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "yrt_host_scene_free": (None, [_vp]),
+    "yrt_scene_upload": (C.c_int, [_vp, C.c_int, C.POINTER(_vp)]),
+    "yrt_scene_device_bytes": (C.c_size_t, [_vp]),
+    "yrt_scene_free": (None, [_vp]),
+    "yrt_render_params_default": (None, [C.POINTER(RenderParams)]),
+    "yrt_image_size": (C.c_int, [_vp, C.POINTER(RenderParams), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "yrt_render": (C.c_int, [_vp, C.POINTER(RenderParams), _vp, C.c_int, _vp]),
+    "yrt_trace_first": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp]),
+    "yrt_trace_any": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int, _vp]),
+    "yrt_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
+    "yrt_tonemap": (C.c_int, [_vp, C.c_int, _vp, C.c_int, _vp]),
+    "yrt_save_image": (C.c_int, [C.c_char_p, _vp, C.c_int, C.c_int]),
+}
+EXPORTS = tuple(_sig)
+
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+class YrtError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        msg = lib.yrt_last_error().decode() or lib.yrt_status_string(status).decode()
+        super().__init__(f"{what}: {lib.yrt_status_string(status).decode()}: {msg}")
+        self.status = status
+
+
+def check(status: int, what: str) -> None:
+    if status != YRT_OK:
+        raise YrtError(status, what)

@@ -1,0 +1,395 @@
+// capi.cpp -- the C-ABI of include/yrt.h over the host scene code and the gfx950
+// kernels. No exceptions cross this boundary: every entry point catches and maps
+// to a status code, with the message kept per thread (yrt_last_error).
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/yrt.h"
+#include "yrt_render.h"
+
+struct yrt_host_scene {
+    yrt::scene scn;
+};
+
+struct yrt_scene {
+    yrt::device_scene* ds = nullptr;
+    unsigned long long* counters = nullptr;  // device, yrt::cnt_count entries
+    void* scratch = nullptr;                 // device staging for host-memory calls
+    size_t scratch_bytes = 0;
+    hipStream_t last_stream = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct hip_failure : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw hip_failure(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        g_last_error.clear();
+        return f();
+    } catch (const hip_failure& e) {
+        g_last_error = e.what();
+        return YRT_ERR_HIP;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "out of memory";
+        return YRT_ERR_OOM;
+    } catch (const std::invalid_argument& e) {
+        g_last_error = e.what();
+        return YRT_ERR_INVALID_ARG;
+    } catch (const std::runtime_error& e) {
+        g_last_error = e.what();
+        std::string m = e.what();
+        if (m.find("unsupported") != std::string::npos || m.find("too deep") != std::string::npos ||
+            m.find("not supported") != std::string::npos || m.find("mixes") != std::string::npos)
+            return YRT_ERR_UNSUPPORTED;
+        if (m.find("hipMalloc") != std::string::npos) return YRT_ERR_OOM;
+        if (m.find("hip") == 0) return YRT_ERR_HIP;
+        return YRT_ERR_IO;
+    } catch (...) {
+        g_last_error = "internal error";
+        return YRT_ERR_INTERNAL;
+    }
+}
+
+void* scratch(yrt_scene* s, size_t bytes) {
+    if (bytes > s->scratch_bytes) {
+        if (s->scratch) hip_check(hipFree(s->scratch), "hipFree");
+        s->scratch = nullptr;
+        s->scratch_bytes = 0;
+        hip_check(hipMalloc(&s->scratch, bytes), "hipMalloc(scratch)");
+        s->scratch_bytes = bytes;
+    }
+    return s->scratch;
+}
+
+struct resolved_window {
+    int W, H, x0, y0, tw, th;
+};
+
+resolved_window resolve(const yrt::device_scene& ds, const yrt_render_params& p) {
+    if (p.resolution <= 0 || p.samples <= 0) throw std::invalid_argument("resolution and samples must be > 0");
+    if (p.camera < 0 || p.camera >= (int)ds.cameras.size()) throw std::invalid_argument("camera index out of range");
+    if (p.band <= 0 || p.band_stride <= 0 || p.band_offset < 0 || p.band_offset >= p.band_stride)
+        throw std::invalid_argument("bad band interleave");
+    const auto& cam = ds.cameras[p.camera];
+    resolved_window r;
+    r.W = p.width > 0 ? p.width : (int)std::round(cam.aspect * p.resolution);  // raytrace.cpp:216
+    r.H = p.resolution;
+    r.x0 = p.x0;
+    r.y0 = p.y0;
+    if (r.x0 < 0 || r.y0 < 0 || r.x0 >= r.W || r.y0 >= r.H) throw std::invalid_argument("window origin outside image");
+    int rows_avail = r.H - r.y0;
+    // local rows available under the band interleave
+    int bands_total = (rows_avail + p.band - 1) / p.band;
+    int my_bands = bands_total > p.band_offset ? (bands_total - p.band_offset + p.band_stride - 1) / p.band_stride : 0;
+    r.tw = p.tile_w > 0 ? p.tile_w : r.W - r.x0;
+    r.th = p.tile_h > 0 ? p.tile_h : my_bands * p.band;
+    if (r.x0 + r.tw > r.W) throw std::invalid_argument("window wider than image");
+    return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yrt_abi_version(void) { return YRT_ABI_VERSION; }
+
+const char* yrt_status_string(int s) {
+    switch (s) {
+        case YRT_OK: return "ok";
+        case YRT_ERR_INVALID_ARG: return "invalid argument";
+        case YRT_ERR_IO: return "i/o or format error";
+        case YRT_ERR_UNSUPPORTED: return "unsupported input";
+        case YRT_ERR_HIP: return "HIP runtime error";
+        case YRT_ERR_NO_DEVICE: return "no GPU device";
+        case YRT_ERR_OOM: return "out of memory";
+        case YRT_ERR_INTERNAL: return "internal error";
+        default: return "unknown status";
+    }
+}
+
+const char* yrt_last_error(void) { return g_last_error.c_str(); }
+
+int yrt_device_count(int* count) {
+    if (!count) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        *count = n;
+        return n > 0 ? YRT_OK : YRT_ERR_NO_DEVICE;
+    });
+}
+
+int yrt_scene_load(const char* path, yrt_host_scene** out) {
+    if (!path || !out) return YRT_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        auto hs = new yrt_host_scene();
+        try {
+            yrt::load_scene_any(path, hs->scn);
+        } catch (...) {
+            delete hs;
+            throw;
+        }
+        *out = hs;
+        return YRT_OK;
+    });
+}
+
+int yrt_scene_save(const yrt_host_scene* hs, const char* path) {
+    if (!hs || !path) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::save_yrtscene(path, hs->scn);
+        return YRT_OK;
+    });
+}
+
+int yrt_host_scene_build_bvh(yrt_host_scene* hs, int equal_num) {
+    if (!hs) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::build_bvh(hs->scn, equal_num != 0);
+        return YRT_OK;
+    });
+}
+
+int yrt_host_scene_save_bvh(const yrt_host_scene* hs, const char* path) {
+    if (!hs || !path) return YRT_ERR_INVALID_ARG;
+    if (!hs->scn.has_bvh) {
+        g_last_error = "scene has no BVH";
+        return YRT_ERR_INVALID_ARG;
+    }
+    return guarded([&] {
+        yrt::save_yrtbvh(path, hs->scn);
+        return YRT_OK;
+    });
+}
+
+int yrt_host_scene_info(const yrt_host_scene* hs, long long* info) {
+    if (!hs || !info) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        const auto& s = hs->scn;
+        long long lights = 0, tris = 0, lines = 0, points = 0, sdepth = 0;
+        for (auto& i : s.instances) {
+            if (i.mat < 0) continue;
+            auto ke = s.materials[i.mat].ke;
+            if (ke.x > 0 && ke.y > 0 && ke.z > 0) lights++;
+        }
+        for (auto& sh : s.shapes) {
+            tris += sh.triangles.size();
+            lines += sh.lines.size();
+            points += sh.points.size();
+            if (s.has_bvh) sdepth = std::max<long long>(sdepth, yrt::bvh_max_depth(sh.bvh));
+        }
+        long long v[12] = {(long long)s.cameras.size(), (long long)s.textures.size(),
+                           (long long)s.materials.size(), (long long)s.shapes.size(),
+                           (long long)s.instances.size(), lights,
+                           s.has_bvh ? (long long)s.bvh.nodes.size() : 0,
+                           s.has_bvh ? (long long)yrt::bvh_max_depth(s.bvh) : 0, sdepth, tris, lines, points};
+        memcpy(info, v, sizeof v);
+        return YRT_OK;
+    });
+}
+
+int yrt_host_image_size(const yrt_host_scene* hs, int camera, int resolution, int* w, int* h) {
+    if (!hs || !w || !h || camera < 0 || camera >= (int)hs->scn.cameras.size() || resolution <= 0)
+        return YRT_ERR_INVALID_ARG;
+    *w = (int)std::round(hs->scn.cameras[camera].aspect * resolution);
+    *h = resolution;
+    return YRT_OK;
+}
+
+void yrt_host_scene_free(yrt_host_scene* hs) { delete hs; }
+
+int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out) {
+    if (!hs || !out) return YRT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        g_last_error = "no HIP device visible";
+        return YRT_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= ndev) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto s = new yrt_scene();
+        try {
+            s->ds = yrt::device_scene_create(hs->scn, device);
+            hip_check(hipMalloc(&s->counters, yrt::cnt_count * sizeof(unsigned long long)), "hipMalloc(counters)");
+            hip_check(hipMemset(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long)), "hipMemset");
+        } catch (...) {
+            yrt_scene_free(s);
+            throw;
+        }
+        *out = s;
+        return YRT_OK;
+    });
+}
+
+size_t yrt_scene_device_bytes(const yrt_scene* s) { return s && s->ds ? s->ds->arena_bytes : 0; }
+
+void yrt_scene_free(yrt_scene* s) {
+    if (!s) return;
+    if (s->ds) hipSetDevice(s->ds->device);
+    if (s->counters) hipFree(s->counters);
+    if (s->scratch) hipFree(s->scratch);
+    yrt::device_scene_destroy(s->ds);
+    delete s;
+}
+
+void yrt_render_params_default(yrt_render_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof *p);
+    p->ambient[0] = p->ambient[1] = p->ambient[2] = 0.1f;  // main(): -a default 0.1
+    p->resolution = 720;                                    // -r default 720
+    p->samples = 1;                                         // -s default 1
+    p->max_depth = 16;
+    p->band = 1;
+    p->band_stride = 1;
+}
+
+int yrt_image_size(const yrt_scene* s, const yrt_render_params* p, int* w, int* h) {
+    if (!s || !p || !w || !h) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto r = resolve(*s->ds, *p);
+        *w = r.W;
+        *h = r.H;
+        return YRT_OK;
+    });
+}
+
+int yrt_render(yrt_scene* s, const yrt_render_params* p, float* out, int mem, void* stream) {
+    if (!s || !p || !out) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto r = resolve(*s->ds, *p);
+        hipStream_t st = (hipStream_t)stream;
+        hip_check(hipSetDevice(s->ds->device), "hipSetDevice");
+        yrt::dev_render_args a = {};
+        a.cam = yrt::make_dev_camera(s->ds->cameras[p->camera]);
+        for (int k = 0; k < 3; k++) a.amb[k] = p->ambient[k];
+        a.width = r.W;
+        a.height = r.H;
+        a.samples = p->samples;
+        a.max_depth = p->max_depth > 0 ? p->max_depth : 16;
+        a.x0 = r.x0;
+        a.tile_w = r.tw;
+        a.y0 = r.y0;
+        a.tile_h = r.th;
+        a.band = p->band;
+        a.band_stride = p->band_stride;
+        a.band_offset = p->band_offset;
+        a.out_stride = p->out_stride > 0 ? p->out_stride : r.tw;
+        if (a.out_stride < r.tw) throw std::invalid_argument("out_stride smaller than the window width");
+        size_t bytes = (size_t)a.out_stride * r.th * 4 * sizeof(float);
+        void* dst = mem == YRT_MEM_DEVICE ? (void*)out : scratch(s, bytes);
+        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
+        hip_check(yrt::launch_render(*s->ds, a, dst, s->counters, p->count_work != 0, st), "render kernel launch");
+        s->last_stream = st;
+        if (mem != YRT_MEM_DEVICE) {
+            hip_check(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+            hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+        }
+        return YRT_OK;
+    });
+}
+
+static int trace_impl(yrt_scene* s, const float* rays, int n, int any, unsigned char* hit, int* inst, int* ei,
+                      float* ew, float* dist, int mem, void* stream) {
+    if (!s || n < 0 || (n && (!rays || !hit))) return YRT_ERR_INVALID_ARG;
+    if (!any && n && (!inst || !ei || !ew || !dist)) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        hipStream_t st = (hipStream_t)stream;
+        hip_check(hipSetDevice(s->ds->device), "hipSetDevice");
+        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
+        s->last_stream = st;
+        if (n == 0) return YRT_OK;
+        if (mem == YRT_MEM_DEVICE) {
+            hip_check(yrt::launch_trace(*s->ds, rays, n, any, hit, inst, ei, ew, dist, s->counters, st), "trace launch");
+            return YRT_OK;
+        }
+        size_t rb = (size_t)n * 8 * 4, hb = ((size_t)n + 255) & ~(size_t)255, ib = (size_t)n * 4, eb = (size_t)n * 16;
+        char* base = (char*)scratch(s, rb + hb + 3 * ib + eb + 1024);
+        float* d_rays = (float*)base;
+        unsigned char* d_hit = (unsigned char*)(base + rb);
+        int* d_inst = (int*)(base + rb + hb);
+        int* d_ei = (int*)(base + rb + hb + ib);
+        float* d_dist = (float*)(base + rb + hb + 2 * ib);
+        float* d_ew = (float*)(base + rb + hb + 3 * ib);
+        hip_check(hipMemcpyAsync(d_rays, rays, rb, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+        hip_check(yrt::launch_trace(*s->ds, d_rays, n, any, d_hit, d_inst, d_ei, d_ew, d_dist, s->counters, st),
+                  "trace launch");
+        hip_check(hipMemcpyAsync(hit, d_hit, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+        if (!any) {
+            hip_check(hipMemcpyAsync(inst, d_inst, ib, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync(ei, d_ei, ib, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync(dist, d_dist, ib, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+            hip_check(hipMemcpyAsync(ew, d_ew, eb, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+        }
+        hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+        return YRT_OK;
+    });
+}
+
+int yrt_trace_first(yrt_scene* s, const float* rays, int n, unsigned char* hit, int* inst, int* ei, float* ew,
+                    float* dist, int mem, void* stream) {
+    return trace_impl(s, rays, n, 0, hit, inst, ei, ew, dist, mem, stream);
+}
+
+int yrt_trace_any(yrt_scene* s, const float* rays, int n, unsigned char* hit, int mem, void* stream) {
+    return trace_impl(s, rays, n, 1, hit, nullptr, nullptr, nullptr, nullptr, mem, stream);
+}
+
+int yrt_last_stats(yrt_scene* s, yrt_stats* out) {
+    if (!s || !out) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        unsigned long long c[yrt::cnt_count];
+        hip_check(hipSetDevice(s->ds->device), "hipSetDevice");
+        hip_check(hipStreamSynchronize(s->last_stream), "hipStreamSynchronize");
+        hip_check(hipMemcpy(c, s->counters, sizeof c, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
+        out->rays = c[yrt::cnt_rays];
+        out->camera_samples = c[yrt::cnt_samples];
+        out->depth_truncated = c[yrt::cnt_depth_truncated];
+        out->stack_overflow = c[yrt::cnt_stack_overflow];
+        out->box_tests = c[yrt::cnt_box_tests];
+        out->instance_entries = c[yrt::cnt_inst_entries];
+        out->prim_tests = c[yrt::cnt_prim_tests];
+        out->shaded_hits = c[yrt::cnt_shaded_hits];
+        out->texture_lookups = c[yrt::cnt_tex_lookups];
+        return YRT_OK;
+    });
+}
+
+int yrt_tonemap(const float* rgba, int n, unsigned char* out, int mem, void* stream) {
+    if (n < 0 || (n && (!rgba || !out))) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        if (mem == YRT_MEM_DEVICE) {
+            hip_check(yrt::launch_tonemap(rgba, n, out, (hipStream_t)stream), "tonemap launch");
+        } else {
+            int h = 1;
+            yrt::tonemap_rgba8(rgba, n, h, out);
+        }
+        return YRT_OK;
+    });
+}
+
+int yrt_save_image(const char* path, const float* rgba, int w, int h) {
+    if (!path || !rgba || w <= 0 || h <= 0) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::save_hdr_or_ldr(path, rgba, w, h);
+        return YRT_OK;
+    });
+}
+
+}  // extern "C"

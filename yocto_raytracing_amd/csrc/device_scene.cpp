@@ -1,0 +1,282 @@
+// device_scene.cpp -- flatten a host scene into the HBM layout of yrt_device.h and
+// upload it as one arena (one hipMalloc, one copy per section).
+//
+// Semantics carried over from the reference's pointer graph (src/scene.h) into
+// indices, so the kernels can reproduce raytrace()/shade() exactly:
+//   * the light list is the instances whose material has ke.x>0 && ke.y>0 && ke.z>0,
+//     in instance order -- the same iteration shade() performs over ALL instances
+//     (raytrace.cpp:121-126), minus the ones that fail the test
+//   * light position = transform_point(frame, pos.front() - p) needs pos.front() of
+//     the light's shape (raytrace.cpp:129-130)
+//   * ns = rs ? 2/pow(rs,4) - 2 : 1e6 (raytrace.cpp:143-144) and the sRGB texel table
+//     fmin(1, pow(c/255, 2.2)) (raytrace.cpp:47-53) are evaluated with the host libm,
+//     the same calls the reference makes per shading point
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "yrt_render.h"
+
+namespace yrt {
+namespace {
+
+float as_float(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+float as_float(int i) { return as_float((uint32_t)i); }
+
+f4 node_lo(const bvh_node& n, uint32_t start) { return {n.bbox.min.x, n.bbox.min.y, n.bbox.min.z, as_float(start)}; }
+f4 node_hi(const bvh_node& n) {
+    uint32_t c = (uint32_t)n.count | (n.isleaf ? leaf_bit : 0u);
+    return {n.bbox.max.x, n.bbox.max.y, n.bbox.max.z, as_float(c)};
+}
+
+void check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct arena_builder {
+    struct section {
+        const void* src;
+        size_t bytes;
+        size_t offset;
+    };
+    std::vector<section> sections;
+    size_t total = 0;
+    size_t add(const void* src, size_t bytes) {
+        size_t off = total;
+        sections.push_back({src, bytes, off});
+        total += (bytes + 255) & ~size_t(255);
+        if (bytes == 0) total += 256;  // keep every pointer distinct and valid
+        return off;
+    }
+};
+
+}  // namespace
+
+dev_camera make_dev_camera(const camera& c) {
+    dev_camera d;
+    d.ox = c.frame.o.x;
+    d.oy = c.frame.o.y;
+    d.oz = c.frame.o.z;
+    d.xx = c.frame.x.x;
+    d.xy = c.frame.x.y;
+    d.xz = c.frame.x.z;
+    vec3f ny = c.frame.y * -1;  // raytrace.cpp:18
+    d.yx = ny.x;
+    d.yy = ny.y;
+    d.yz = ny.z;
+    d.zx = c.frame.z.x;
+    d.zy = c.frame.z.y;
+    d.zz = c.frame.z.z;
+    d.h = 2.0f * c.focus * std::tan(c.fovy / 2.0f);  // raytrace.cpp:21 (tanf)
+    d.w = d.h * c.aspect;
+    d.focus = c.focus;
+    return d;
+}
+
+device_scene* device_scene_create(const scene& scn, int device) {
+    if (!scn.has_bvh) throw std::runtime_error("scene has no BVH (call build_bvh first)");
+    if (scn.cameras.empty()) throw std::runtime_error("scene has no camera");
+    if (scn.instances.empty()) throw std::runtime_error("scene has no instances");
+
+    auto ds = new device_scene();
+    ds->device = device;
+    ds->cameras = scn.cameras;
+    ds->top_depth = bvh_max_depth(scn.bvh);
+    for (auto& s : scn.shapes) ds->shape_depth = std::max(ds->shape_depth, bvh_max_depth(s.bvh));
+    if (ds->top_depth > top_stack_cap || ds->shape_depth > shape_stack_cap) {
+        int td = ds->top_depth, sd = ds->shape_depth;
+        delete ds;
+        throw std::runtime_error("BVH too deep for the kernel stacks (instance " + std::to_string(td) +
+                                 ", shape " + std::to_string(sd) + ")");
+    }
+
+    // ---- shapes: nodes, leaf-ordered primitives, elements, vertices ----
+    std::vector<f4> snodes, sprims, vpos, vnorm;
+    std::vector<f2> vuv;
+    std::vector<i4> shapes, elems;
+    for (size_t si = 0; si < scn.shapes.size(); si++) {
+        const shape& s = scn.shapes[si];
+        int kinds = (!s.triangles.empty()) + (!s.lines.empty()) + (!s.points.empty());
+        if (kinds > 1)
+            throw std::runtime_error("shape " + s.name + " mixes primitive types (unsupported)");
+        int kind = !s.triangles.empty() ? kind_triangles
+                   : !s.lines.empty()   ? kind_lines
+                   : !s.points.empty()  ? kind_points
+                                        : kind_empty;
+        int node_base = (int)snodes.size() / 2;
+        int prim_base = (int)sprims.size() / 3;
+        int elem_base = (int)elems.size();
+        int vert_base = (int)vpos.size();
+        for (auto& n : s.bvh.nodes) {
+            uint32_t start = n.isleaf ? n.start + prim_base : n.start + node_base;
+            snodes.push_back(node_lo(n, start));
+            snodes.push_back(node_hi(n));
+        }
+        for (int ei : s.bvh.leaf_prims) {
+            if (kind == kind_triangles) {
+                vec3i t = s.triangles[ei];
+                vec3f v0 = s.pos[t.x], e1 = s.pos[t.y] - v0, e2 = s.pos[t.z] - v0;
+                sprims.push_back({v0.x, v0.y, v0.z, as_float(ei)});
+                sprims.push_back({e1.x, e1.y, e1.z, 0});
+                sprims.push_back({e2.x, e2.y, e2.z, 0});
+            } else if (kind == kind_lines) {
+                vec2i l = s.lines[ei];
+                vec3f v0 = s.pos[l.x], v1 = s.pos[l.y];
+                sprims.push_back({v0.x, v0.y, v0.z, as_float(ei)});
+                sprims.push_back({v1.x, v1.y, v1.z, s.radius[l.x]});
+                sprims.push_back({s.radius[l.y], 0, 0, 0});
+            } else {
+                int p = s.points[ei];
+                vec3f v = s.pos[p];
+                sprims.push_back({v.x, v.y, v.z, as_float(ei)});
+                sprims.push_back({s.radius[p], 0, 0, 0});
+                sprims.push_back({0, 0, 0, 0});
+            }
+        }
+        if (kind == kind_triangles)
+            for (auto t : s.triangles) elems.push_back({t.x + vert_base, t.y + vert_base, t.z + vert_base, 0});
+        else if (kind == kind_lines)
+            for (auto l : s.lines) elems.push_back({l.x + vert_base, l.y + vert_base, -1, 0});
+        else if (kind == kind_points)
+            for (auto p : s.points) elems.push_back({p + vert_base, -1, -1, 0});
+        for (size_t v = 0; v < s.pos.size(); v++) {
+            vec3f p = s.pos[v];
+            vec3f n = v < s.norm.size() ? s.norm[v] : vec3f{0, 0, 0};
+            vec2f t = v < s.texcoord.size() ? s.texcoord[v] : vec2f{0, 0};
+            vpos.push_back({p.x, p.y, p.z, 0});
+            vnorm.push_back({n.x, n.y, n.z, 0});
+            vuv.push_back({t.x, t.y});
+        }
+        shapes.push_back({node_base, kind, elem_base, vert_base});
+    }
+
+    // ---- instance level: nodes + instances permuted into leaf order ----
+    std::vector<f4> tnodes, tinst;
+    for (auto& n : scn.bvh.nodes) {
+        tnodes.push_back(node_lo(n, n.start));
+        tnodes.push_back(node_hi(n));
+    }
+    for (int ii : scn.bvh.leaf_prims) {
+        const instance& ist = scn.instances[ii];
+        if (ist.mat < 0 || ist.mat >= (int)scn.materials.size())
+            throw std::runtime_error("instance " + ist.name + " has no material");
+        const frame3f& f = ist.frame;
+        tinst.push_back({f.x.x, f.x.y, f.x.z, as_float(ist.shp)});
+        tinst.push_back({f.y.x, f.y.y, f.y.z, as_float(ii)});
+        tinst.push_back({f.z.x, f.z.y, f.z.z, as_float(ist.mat)});
+        tinst.push_back({f.o.x, f.o.y, f.o.z, 0});
+    }
+
+    // ---- materials, lights, textures ----
+    std::vector<f4> mats, lights;
+    for (auto& m : scn.materials) {
+        float rs = m.rs;
+        float ns = (rs) ? 2 / std::pow(rs, 4.0f) - 2 : 1e6f;  // raytrace.cpp:144
+        int flags = (m.kr.x > 0.0f || m.kr.y > 0.0f || m.kr.z > 0.0f) ? mat_reflective : 0;
+        for (int t : {m.kd_txt, m.ks_txt}) {
+            if (t >= (int)scn.textures.size() || (t >= 0 && scn.textures[t].pixels.empty()))
+                throw std::runtime_error("material " + m.name + " references a missing texture");
+        }
+        mats.push_back({m.kd.x, m.kd.y, m.kd.z, ns});
+        mats.push_back({m.ks.x, m.ks.y, m.ks.z, as_float(m.kd_txt)});
+        mats.push_back({m.kr.x, m.kr.y, m.kr.z, as_float(m.ks_txt)});
+        mats.push_back({m.ke.x, m.ke.y, m.ke.z, as_float(flags)});
+    }
+    for (auto& ist : scn.instances) {
+        if (ist.mat < 0) continue;
+        vec3f ke = scn.materials[ist.mat].ke;
+        if (!(ke.x > 0.0f && ke.y > 0.0f && ke.z > 0.0f)) continue;
+        const shape& s = scn.shapes[ist.shp];
+        if (s.pos.empty()) throw std::runtime_error("light " + ist.name + " has no vertex");
+        const frame3f& f = ist.frame;
+        vec3f p0 = s.pos.front();
+        lights.push_back({f.x.x, f.x.y, f.x.z, 0});
+        lights.push_back({f.y.x, f.y.y, f.y.z, 0});
+        lights.push_back({f.z.x, f.z.y, f.z.z, 0});
+        lights.push_back({f.o.x, f.o.y, f.o.z, 0});
+        lights.push_back({p0.x, p0.y, p0.z, 0});
+        lights.push_back({ke.x, ke.y, ke.z, 0});
+    }
+    std::vector<uint32_t> texels;
+    std::vector<i4> texinfo;
+    for (auto& t : scn.textures) {
+        texinfo.push_back({(int)texels.size(), t.width, t.height, 0});
+        for (auto& p : t.pixels)
+            texels.push_back((uint32_t)p.x | (uint32_t)p.y << 8 | (uint32_t)p.z << 16 | (uint32_t)p.w << 24);
+    }
+    std::vector<float> srgb(256);
+    for (int c = 0; c < 256; c++) {
+        float r = (float)(unsigned char)c;
+        srgb[c] = std::fmin(1.0f, std::pow(r / 255.0f, 2.2f));  // raytrace.cpp:51
+    }
+
+    // ---- upload ----
+    arena_builder ab;
+    size_t o_tnodes = ab.add(tnodes.data(), tnodes.size() * sizeof(f4));
+    size_t o_tinst = ab.add(tinst.data(), tinst.size() * sizeof(f4));
+    size_t o_snodes = ab.add(snodes.data(), snodes.size() * sizeof(f4));
+    size_t o_sprims = ab.add(sprims.data(), sprims.size() * sizeof(f4));
+    size_t o_shapes = ab.add(shapes.data(), shapes.size() * sizeof(i4));
+    size_t o_elems = ab.add(elems.data(), elems.size() * sizeof(i4));
+    size_t o_vpos = ab.add(vpos.data(), vpos.size() * sizeof(f4));
+    size_t o_vnorm = ab.add(vnorm.data(), vnorm.size() * sizeof(f4));
+    size_t o_vuv = ab.add(vuv.data(), vuv.size() * sizeof(f2));
+    size_t o_mats = ab.add(mats.data(), mats.size() * sizeof(f4));
+    size_t o_lights = ab.add(lights.data(), lights.size() * sizeof(f4));
+    size_t o_texels = ab.add(texels.data(), texels.size() * sizeof(uint32_t));
+    size_t o_texinfo = ab.add(texinfo.data(), texinfo.size() * sizeof(i4));
+    size_t o_srgb = ab.add(srgb.data(), srgb.size() * sizeof(float));
+
+    try {
+        check(hipSetDevice(device), "hipSetDevice");
+        check(hipMalloc(&ds->arena, ab.total), "hipMalloc(scene arena)");
+        ds->arena_bytes = ab.total;
+        for (auto& s : ab.sections)
+            if (s.bytes)
+                check(hipMemcpy((char*)ds->arena + s.offset, s.src, s.bytes, hipMemcpyHostToDevice),
+                      "hipMemcpy(scene)");
+    } catch (...) {
+        device_scene_destroy(ds);
+        throw;
+    }
+    char* base = (char*)ds->arena;
+    dev_scene_view& v = ds->view;
+    v.tnodes = (const f4*)(base + o_tnodes);
+    v.tinst = (const f4*)(base + o_tinst);
+    v.snodes = (const f4*)(base + o_snodes);
+    v.sprims = (const f4*)(base + o_sprims);
+    v.shapes = (const i4*)(base + o_shapes);
+    v.elems = (const i4*)(base + o_elems);
+    v.vpos = (const f4*)(base + o_vpos);
+    v.vnorm = (const f4*)(base + o_vnorm);
+    v.vuv = (const f2*)(base + o_vuv);
+    v.mats = (const f4*)(base + o_mats);
+    v.lights = (const f4*)(base + o_lights);
+    v.texels = (const uint32_t*)(base + o_texels);
+    v.texinfo = (const i4*)(base + o_texinfo);
+    v.srgb = (const float*)(base + o_srgb);
+    v.nlights = (int)lights.size() / 6;
+    v.ntnodes = (int)tnodes.size() / 2;
+    ds->ntnodes = tnodes.size() / 2;
+    ds->nsnodes = snodes.size() / 2;
+    ds->nsprims = sprims.size() / 3;
+    ds->ninst = tinst.size() / 4;
+    return ds;
+}
+
+void device_scene_destroy(device_scene* ds) {
+    if (!ds) return;
+    if (ds->arena) {
+        hipSetDevice(ds->device);
+        hipFree(ds->arena);
+    }
+    delete ds;
+}
+
+}  // namespace yrt

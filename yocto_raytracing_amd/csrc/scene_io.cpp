@@ -1,0 +1,240 @@
+// scene_io.cpp -- .yrtscene / .yrtbvh interchange formats and image output.
+//
+// .yrtscene (gzip, little-endian; spec DESIGN.md §3) carries exactly the arrays
+// raytrace() reads from a loaded reference scene (src/scene.h:26-155): cameras,
+// 8-bit textures, materials (ke kd ks kr rs kd_txt ks_txt), shapes (pos norm
+// texcoord radius points lines triangles) and instances (frame shape material).
+// The reference harness (oracle/ref_harness.cpp) writes the same format from the
+// reference's own loader, so product and reference scenes compare byte-for-byte.
+//
+// Image output restates tonemap + save_hdr_or_ldr (src/image.cpp:55-88).
+#include <zlib.h>
+
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "yrt_scene.h"
+
+namespace yrt {
+namespace {
+
+struct gz_writer {
+    gzFile f;
+    explicit gz_writer(const std::string& p) : f(gzopen(p.c_str(), "wb6")) {
+        if (!f) throw std::runtime_error("cannot write " + p);
+    }
+    ~gz_writer() { gzclose(f); }
+    void raw(const void* p, size_t n) {
+        if (n && gzwrite(f, p, (unsigned)n) != (int)n) throw std::runtime_error("gzwrite failed");
+    }
+    void u32(uint32_t v) { raw(&v, 4); }
+    void i32(int32_t v) { raw(&v, 4); }
+    template <class T>
+    void vec(const std::vector<T>& v) {
+        u32((uint32_t)v.size());
+        raw(v.data(), v.size() * sizeof(T));
+    }
+};
+
+struct gz_reader {
+    gzFile f;
+    std::string path;
+    explicit gz_reader(const std::string& p) : f(gzopen(p.c_str(), "rb")), path(p) {
+        if (!f) throw std::runtime_error("cannot open filename " + p);
+    }
+    ~gz_reader() { gzclose(f); }
+    void raw(void* p, size_t n) {
+        if (n && gzread(f, p, (unsigned)n) != (int)n)
+            throw std::runtime_error("truncated scene file " + path);
+    }
+    uint32_t u32() {
+        uint32_t v;
+        raw(&v, 4);
+        return v;
+    }
+    int32_t i32() {
+        int32_t v;
+        raw(&v, 4);
+        return v;
+    }
+    template <class T>
+    void vec(std::vector<T>& v, uint32_t limit = 1u << 28) {
+        uint32_t n = u32();
+        if (n > limit) throw std::runtime_error("corrupt scene file " + path);
+        v.resize(n);
+        raw(v.data(), (size_t)n * sizeof(T));
+    }
+};
+
+}  // namespace
+
+void save_yrtscene(const std::string& filename, const scene& scn) {
+    gz_writer o(filename);
+    o.raw("YRTSCN1", 8);
+    o.u32((uint32_t)scn.cameras.size());
+    for (auto& c : scn.cameras) {
+        o.raw(&c.frame, 48);
+        o.raw(&c.fovy, 4);
+        o.raw(&c.aspect, 4);
+        o.raw(&c.aperture, 4);
+        o.raw(&c.focus, 4);
+    }
+    o.u32((uint32_t)scn.textures.size());
+    for (auto& t : scn.textures) {
+        o.i32(t.width);
+        o.i32(t.height);
+        o.raw(t.pixels.data(), t.pixels.size() * 4);
+    }
+    o.u32((uint32_t)scn.materials.size());
+    for (auto& m : scn.materials) {
+        o.raw(&m.ke, 12);
+        o.raw(&m.kd, 12);
+        o.raw(&m.ks, 12);
+        o.raw(&m.kr, 12);
+        o.raw(&m.rs, 4);
+        o.i32(m.kd_txt);
+        o.i32(m.ks_txt);
+    }
+    o.u32((uint32_t)scn.shapes.size());
+    for (auto& s : scn.shapes) {
+        o.vec(s.pos);
+        o.vec(s.norm);
+        o.vec(s.texcoord);
+        o.vec(s.radius);
+        o.vec(s.points);
+        o.vec(s.lines);
+        o.vec(s.triangles);
+    }
+    o.u32((uint32_t)scn.instances.size());
+    for (auto& i : scn.instances) {
+        o.raw(&i.frame, 48);
+        o.i32(i.shp);
+        o.i32(i.mat);
+    }
+}
+
+void load_yrtscene(const std::string& filename, scene& scn) {
+    gz_reader in(filename);
+    char magic[8];
+    in.raw(magic, 8);
+    if (memcmp(magic, "YRTSCN1", 8) != 0) throw std::runtime_error("not a .yrtscene file: " + filename);
+    scn = scene();
+    scn.cameras.resize(in.u32());
+    for (auto& c : scn.cameras) {
+        in.raw(&c.frame, 48);
+        in.raw(&c.fovy, 4);
+        in.raw(&c.aspect, 4);
+        in.raw(&c.aperture, 4);
+        in.raw(&c.focus, 4);
+    }
+    scn.textures.resize(in.u32());
+    for (auto& t : scn.textures) {
+        t.width = in.i32();
+        t.height = in.i32();
+        if (t.width < 0 || t.height < 0 || (size_t)t.width * t.height > (1u << 28))
+            throw std::runtime_error("corrupt texture in " + filename);
+        t.pixels.resize((size_t)t.width * t.height);
+        in.raw(t.pixels.data(), t.pixels.size() * 4);
+    }
+    scn.materials.resize(in.u32());
+    for (auto& m : scn.materials) {
+        in.raw(&m.ke, 12);
+        in.raw(&m.kd, 12);
+        in.raw(&m.ks, 12);
+        in.raw(&m.kr, 12);
+        in.raw(&m.rs, 4);
+        m.kd_txt = in.i32();
+        m.ks_txt = in.i32();
+    }
+    scn.shapes.resize(in.u32());
+    for (auto& s : scn.shapes) {
+        in.vec(s.pos);
+        in.vec(s.norm);
+        in.vec(s.texcoord);
+        in.vec(s.radius);
+        in.vec(s.points);
+        in.vec(s.lines);
+        in.vec(s.triangles);
+    }
+    scn.instances.resize(in.u32());
+    for (auto& i : scn.instances) {
+        in.raw(&i.frame, 48);
+        i.shp = in.i32();
+        i.mat = in.i32();
+        if (i.shp < 0 || i.shp >= (int)scn.shapes.size())
+            throw std::runtime_error("instance with invalid shape in " + filename);
+    }
+}
+
+void load_scene_any(const std::string& filename, scene& scn) {
+    auto dot = filename.rfind('.');
+    std::string ext = dot == std::string::npos ? "" : filename.substr(dot);
+    if (ext == ".obj" || ext == ".OBJ")
+        load_obj_scene(filename, scn);
+    else
+        load_yrtscene(filename, scn);
+}
+
+void save_yrtbvh(const std::string& filename, const scene& scn) {
+    gz_writer o(filename);
+    o.raw("YRTBVH1", 8);
+    o.u32((uint32_t)scn.shapes.size());
+    for (auto& s : scn.shapes) {
+        o.vec(s.bvh.nodes);
+        o.vec(s.bvh.leaf_prims);
+    }
+    o.vec(scn.bvh.nodes);
+    o.vec(scn.bvh.leaf_prims);
+}
+
+// image.cpp:55-77 with exposure 0 (pow(2,0) == 1 exactly), no filmic, srgb on
+void tonemap_rgba8(const float* px, int w, int h, unsigned char* out) {
+    for (size_t k = 0; k < (size_t)w * h; k++) {
+        float r = std::pow(px[k * 4 + 0], 1 / 2.2f);
+        float g = std::pow(px[k * 4 + 1], 1 / 2.2f);
+        float b = std::pow(px[k * 4 + 2], 1 / 2.2f);
+        float a = px[k * 4 + 3];
+        out[k * 4 + 0] = (unsigned char)(sclamp(r, 0.0f, 1.0f) * 255);
+        out[k * 4 + 1] = (unsigned char)(sclamp(g, 0.0f, 1.0f) * 255);
+        out[k * 4 + 2] = (unsigned char)(sclamp(b, 0.0f, 1.0f) * 255);
+        out[k * 4 + 3] = (unsigned char)(sclamp(a, 0.0f, 1.0f) * 255);
+    }
+}
+
+void save_hdr_or_ldr(const std::string& filename, const float* px, int w, int h) {
+    FILE* f = fopen(filename.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + filename);
+    bool hdr = filename.size() >= 4 && filename.substr(filename.size() - 4) == ".hdr";
+    if (hdr) {
+        // Radiance RGBE, flat (uncompressed) scanlines
+        fprintf(f, "#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y %d +X %d\n", h, w);
+        std::vector<unsigned char> row((size_t)w * 4);
+        for (int j = 0; j < h; j++) {
+            for (int i = 0; i < w; i++) {
+                const float* p = px + ((size_t)j * w + i) * 4;
+                float m = std::fmax(p[0], std::fmax(p[1], p[2]));
+                unsigned char* e = &row[(size_t)i * 4];
+                if (!(m >= 1e-32f)) {
+                    e[0] = e[1] = e[2] = e[3] = 0;
+                } else {
+                    int ex;
+                    float n = std::frexp(m, &ex) * 256.0f / m;
+                    e[0] = (unsigned char)(p[0] * n);
+                    e[1] = (unsigned char)(p[1] * n);
+                    e[2] = (unsigned char)(p[2] * n);
+                    e[3] = (unsigned char)(ex + 128);
+                }
+            }
+            fwrite(row.data(), 1, row.size(), f);
+        }
+    } else {
+        std::vector<unsigned char> ldr((size_t)w * h * 4), png;
+        tonemap_rgba8(px, w, h, ldr.data());
+        png_encode_rgba8(ldr.data(), w, h, png);
+        fwrite(png.data(), 1, png.size(), f);
+    }
+    fclose(f);
+}
+
+}  // namespace yrt

@@ -1,0 +1,97 @@
+// yrt_device.h -- HBM layout of a scene on one MI355X, shared by
+// the host flattener (device_scene.cpp) and the gfx950 kernels (render.hip).
+//
+// Everything is 16-byte records so each fetch is one global_load_dwordx4:
+//   tnodes  2 x f4 per instance-BVH node  {min.xyz, start} {max.xyz, count|leaf<<31}
+//   tinst   4 x f4 per instance-BVH leaf slot (instances permuted to leaf order)
+//           {frame.x, shape} {frame.y, instance id} {frame.z, material} {frame.o, -}
+//   snodes  2 x f4 per shape-BVH node, all shapes concatenated, child/leaf indices absolute
+//   sprims  3 x f4 per shape-BVH leaf slot (primitives permuted to leaf order)
+//           triangle {v0, ei} {v1-v0, -} {v2-v0, -}   (the reference's e1/e2, scene.cpp:232-233)
+//           line     {v0, ei} {v1, r0}  {r1, -, -, -}
+//           point    {p, ei}  {r, -, -, -} {-}
+//   shapes  i4 per shape {root node, kind, elem base, vertex base}
+//   elems   i4 per element (original index order) with absolute vertex indices
+//   vpos/vnorm f4, vuv f2 per vertex
+//   mats    4 x f4 {kd, ns} {ks, kd_txt} {kr, ks_txt} {ke, flags}
+//   lights  6 x f4 {frame.x} {frame.y} {frame.z} {frame.o} {pos0 of the light shape} {ke}
+//   texels  RGBA8 of every texture; texinfo i4 {offset, width, height, -}
+//   srgb    256 floats: fmin(1, pow(c/255, 2.2)) (raytrace.cpp:51-53) precomputed on the host
+#pragma once
+
+#include <stdint.h>
+
+namespace yrt {
+
+struct alignas(16) f4 {
+    float x, y, z, w;
+};
+struct alignas(16) i4 {
+    int x, y, z, w;
+};
+struct alignas(8) f2 {
+    float x, y;
+};
+
+enum shape_kind : int { kind_triangles = 0, kind_lines = 1, kind_points = 2, kind_empty = 3 };
+enum mat_flags : int { mat_reflective = 1 };
+
+constexpr uint32_t leaf_bit = 0x80000000u;
+
+struct dev_scene_view {
+    const f4* tnodes;
+    const f4* tinst;
+    const f4* snodes;
+    const f4* sprims;
+    const i4* shapes;
+    const i4* elems;
+    const f4* vpos;
+    const f4* vnorm;
+    const f2* vuv;
+    const f4* mats;
+    const f4* lights;
+    const uint32_t* texels;
+    const i4* texinfo;
+    const float* srgb;
+    int nlights;
+    int ntnodes;
+};
+
+// per-frame camera constants, hoisted from eval_camera (raytrace.cpp:16-24); tanf is
+// evaluated on the host with the same libm call the reference makes
+struct dev_camera {
+    float ox, oy, oz;
+    float xx, xy, xz;
+    float yx, yy, yz;  // frame.y * -1
+    float zx, zy, zz;
+    float h, w, focus;
+};
+
+struct dev_render_args {
+    dev_camera cam;
+    float amb[3];
+    int width, height;  // full image size (uv denominators, raytrace.cpp:237-238)
+    int samples;        // per axis
+    int max_depth;      // trace_first calls per camera sample (reference: unbounded)
+    int x0, tile_w;     // columns [x0, x0+tile_w)
+    int y0, tile_h;     // local rows [0, tile_h): image row = y0 + band interleave
+    int band, band_stride, band_offset;  // local band b -> image band b*band_stride+band_offset
+    int out_stride;     // floats4 per output row
+};
+
+// device counters (u64): rays, camera samples, depth-truncated paths, stack overflows,
+// then the optional work counters (box tests, instance entries, primitive tests, hits)
+enum counter_index {
+    cnt_rays = 0,
+    cnt_samples = 1,
+    cnt_depth_truncated = 2,
+    cnt_stack_overflow = 3,
+    cnt_box_tests = 4,
+    cnt_inst_entries = 5,
+    cnt_prim_tests = 6,
+    cnt_shaded_hits = 7,
+    cnt_tex_lookups = 8,
+    cnt_count = 16
+};
+
+}  // namespace yrt
