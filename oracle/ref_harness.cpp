@@ -333,4 +333,14 @@ int ref_camera_ray(void* vscn, int resolution, int samples, int i, int j, int ii
     return 0;
 }
 
+// The reference's own PNG loader (image.cpp:25-35, stb_image) for its shipped images.
+// Call with out == nullptr to get the size, then again with a w*h*4 buffer.
+int ref_load_image4b(const char* path, int* w, int* h, unsigned char* out) {
+    auto img = load_image4b(path);
+    *w = img.width;
+    *h = img.height;
+    if (out) memcpy(out, img.pixels.data(), img.pixels.size() * 4);
+    return img.pixels.empty() ? -1 : 0;
+}
+
 }  // extern "C"

@@ -1,0 +1,132 @@
+"""Shared test helpers: the oracle binding (test infrastructure), fixture paths and
+image metrics. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+touch oracle/."""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import subprocess
+from functools import lru_cache
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+GOLDEN = ROOT / "tests" / "golden"
+SCENES = GOLDEN / "scenes"
+SCENE_NAMES = ("basic", "simple", "refl", "instance10000")
+REFERENCE = Path("/root/reference")
+REF_OBJ = {
+    "basic": REFERENCE / "in/basic_pointlight/basic_pointlight.obj",
+    "simple": REFERENCE / "in/simple_pointlight/simple_pointlight.obj",
+    "refl": REFERENCE / "in/refl_pointlight/refl_pointlight.obj",
+    "instance10000": REFERENCE / "in/instance10000_pointlight/instance10000_pointlight.obj",
+}
+
+# Per-channel float tolerance of the GPU path against the reference / oracle
+# (DESIGN.md §6): the only libm call left on the device is pow() in the specular
+# term; everything else is bit-exact by construction.
+ATOL = 1e-6
+RTOL = 2e-6
+
+
+def scene_path(name: str) -> Path:
+    return SCENES / f"{name}.yrtscene"
+
+
+def digests() -> dict:
+    return json.loads((GOLDEN / "ref_digests.json").read_text())
+
+
+@lru_cache(maxsize=None)
+def oracle_lib():
+    so = ROOT / "oracle" / "liboracle.so"
+    if not so.exists():
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), "liboracle.so"], check=True,
+                       capture_output=True)
+    lib = C.CDLL(str(so))
+    lib.oracle_load.restype = C.c_void_p
+    lib.oracle_load.argtypes = [C.c_char_p]
+    lib.oracle_free.argtypes = [C.c_void_p]
+    lib.oracle_write_bvh.argtypes = [C.c_void_p, C.c_char_p]
+    lib.oracle_image_size.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    lib.oracle_render_rows.restype = C.c_longlong
+    lib.oracle_render_rows.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    lib.oracle_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 5
+    lib.oracle_camera_ray.argtypes = [C.c_void_p] + [C.c_int] * 8 + [C.c_void_p]
+    return lib
+
+
+class Oracle:
+    """CPU restatement of the reference (oracle/oracle.c) on a .yrtscene file."""
+
+    def __init__(self, name_or_path):
+        p = scene_path(name_or_path) if name_or_path in SCENE_NAMES else Path(name_or_path)
+        self.lib = oracle_lib()
+        self.h = self.lib.oracle_load(str(p).encode())
+        if not self.h:
+            raise RuntimeError(f"oracle could not load {p}")
+
+    def __del__(self):
+        try:
+            self.lib.oracle_free(self.h)
+        except Exception:
+            pass
+
+    def image_size(self, resolution, camera=0):
+        w, h = C.c_int(), C.c_int()
+        self.lib.oracle_image_size(self.h, camera, resolution, C.byref(w), C.byref(h))
+        return w.value, h.value
+
+    def render(self, resolution, samples, amb=0.1, rows=None, x0=0, ncols=None, width=0, max_depth=0,
+               camera=0):
+        W, H = self.image_size(resolution, camera)
+        if width:
+            W = width
+        rows = np.arange(H, dtype=np.int32) if rows is None else np.ascontiguousarray(rows, np.int32)
+        ncols = W - x0 if ncols is None else ncols
+        out = np.zeros((len(rows), ncols, 4), np.float32)
+        trunc = C.c_longlong(0)
+        n = self.lib.oracle_render_rows(self.h, amb, camera, resolution, width, samples, max_depth,
+                                        rows.ctypes.data, len(rows), x0, ncols, out.ctypes.data,
+                                        C.byref(trunc))
+        if n < 0:
+            raise RuntimeError("oracle render failed")
+        return out, int(n), int(trunc.value)
+
+    def trace(self, rays, any_hit=False):
+        rays = np.ascontiguousarray(rays, np.float32)
+        n = len(rays)
+        hit = np.zeros(n, np.uint8)
+        inst = np.zeros(n, np.int32)
+        ei = np.zeros(n, np.int32)
+        ew = np.zeros((n, 4), np.float32)
+        dist = np.zeros(n, np.float32)
+        self.lib.oracle_trace(self.h, rays.ctypes.data, n, 1 if any_hit else 0, hit.ctypes.data,
+                              inst.ctypes.data, ei.ctypes.data, ew.ctypes.data, dist.ctypes.data)
+        return {"hit": hit.astype(bool), "inst": inst, "ei": ei, "ew": ew, "dist": dist}
+
+
+def tonemap_ref(img: np.ndarray) -> np.ndarray:
+    """tonemap (image.cpp:55-77) in numpy: pow(x, 1/2.2), select clamp, truncate *255."""
+    x = img[..., :3].astype(np.float32)
+    with np.errstate(invalid="ignore"):
+        g = np.power(x, np.float32(1 / 2.2)).astype(np.float32)
+    g = np.where(g > 0, g, np.float32(0))  # max(x, 0): NaN -> 0
+    g = np.where(g < 1, g, np.float32(1))
+    return (g * np.float32(255)).astype(np.uint8)
+
+
+def psnr_u8(a: np.ndarray, b: np.ndarray) -> float:
+    d = a.astype(np.float64) - b.astype(np.float64)
+    mse = float(np.mean(d * d))
+    return float("inf") if mse == 0 else 10 * np.log10(255.0 ** 2 / mse)
+
+
+def close_mask(a: np.ndarray, b: np.ndarray, atol=ATOL, rtol=RTOL) -> np.ndarray:
+    return np.abs(a.astype(np.float64) - b.astype(np.float64)) <= atol + rtol * np.abs(b.astype(np.float64))
+
+
+def have_reference() -> bool:
+    return (REFERENCE / "src" / "raytrace.cpp").exists() and (ROOT / "oracle/_ref/libyrtref.so").exists()
