@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--samples", type=int, default=8, help="per axis: 8 -> 64 spp")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    p.add_argument("--algorithm", default="wavefront", choices=("wavefront", "megakernel", "wavefront_lane"))
     return p.parse_args()
 
 
@@ -142,7 +143,8 @@ def main():
     yrt.build_bvh(scn)
     ds = scn.upload(local)
 
-    params = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=(BAND, world, rank))
+    params = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=(BAND, world, rank),
+                               algorithm=a.algorithm)
     W, H = ds.image_size(params)
     nbands = (H + BAND - 1) // BAND
     bands_per_rank = (nbands + world - 1) // world
@@ -164,22 +166,29 @@ def main():
 
     # untimed instrumented pass: algorithmic work counts for the roofline bytes
     pc = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=(BAND, world, rank),
-                           count_work=True)
+                           count_work=True, algorithm=a.algorithm)
     pc.tile_h = local_rows
     ds.render_into(pc, shard.data_ptr(), stream=stream.cuda_stream)
     work = ds.last_stats()
-    alg_bytes = (work["box_tests"] * BYTES_BOX + work["instance_entries"] * BYTES_INST +
-                 work["prim_tests"] * BYTES_PRIM + work["shaded_hits"] * BYTES_HIT +
-                 work["texture_lookups"] * BYTES_TEX + local_rows * W * BYTES_PIXEL)
+    # per kernel phase: SURVEY §8d cost model on the phase's own traversal counts, plus
+    # the wavefront buffers the phase reads/writes (shadow: 16 B hit point in, 1 B out)
+    sh = {k: work[f"shadow_{k}"] for k in ("box_tests", "instance_entries", "prim_tests", "rays")}
+    alg = {
+        "shadow": sh["box_tests"] * BYTES_BOX + sh["instance_entries"] * BYTES_INST +
+                  sh["prim_tests"] * BYTES_PRIM + sh["rays"] * 17,
+        "primary": (work["box_tests"] - sh["box_tests"]) * BYTES_BOX +
+                   (work["instance_entries"] - sh["instance_entries"]) * BYTES_INST +
+                   (work["prim_tests"] - sh["prim_tests"]) * BYTES_PRIM + work["camera_samples"] * 36,
+        "megakernel": work["box_tests"] * BYTES_BOX + work["instance_entries"] * BYTES_INST +
+                      work["prim_tests"] * BYTES_PRIM + work["shaded_hits"] * BYTES_HIT +
+                      work["texture_lookups"] * BYTES_TEX + local_rows * W * BYTES_PIXEL,
+    }
+    kernel_names = {"shadow": "k_shadow<false,u16>", "primary": "k_primary<false,u16>",
+                    "megakernel": "render_kernel<false>"}
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-
-    def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
+    def step(timing=0):
+        params.timing = timing
         ds.render_into(params, shard.data_ptr(), stream=stream.cuda_stream)
-        if i is not None:
-            ev[i][1].record(stream)
         if world > 1:
             dist.all_gather_into_tensor(gathered, shard)
         torch.index_select(gathered, 0, perm, out=frame)
@@ -191,31 +200,38 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(i)
+        # HIP events around every kernel launch, on the launch stream (library-side)
+        step(timing=1 if i == 0 else 2)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ds.last_stats()
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    phases = ds.last_timings()  # {phase: (ms over the K steps, launches)}
+    dom = max(phases, key=lambda k: phases[k][0])
+    dom_ms = phases[dom][0] / a.steps  # per frame; one launch per frame at N=1 (one chunk)
+    dom_launches = phases[dom][1] / a.steps
+    render_ms = sum(v[0] for v in phases.values()) / a.steps
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, dom_ms, render_ms], dtype=torch.float64, device=dev)
     rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
+    elapsed, dom_ms, render_ms = float(t[0]), float(t[1]), float(t[2])
     total_rays, total_samples = float(rays[0]), float(rays[1])
+    alg_bytes = alg.get(dom)
 
     if rank == 0:
-        achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+        # per launch: algorithmic bytes of one frame's launch(es) / their mean duration
+        achieved = (alg_bytes / dom_launches) / (dom_ms / dom_launches / 1e3) / 1e9 if alg_bytes else None
         traffic = None
         tj = Path(a.traffic_json)
         if tj.exists():
             try:
                 tr = json.loads(tj.read_text())
-                if tr.get("config") == f"{a.scene}-r{a.resolution}-s{a.samples}-n{world}":
-                    traffic = tr.get("hbm_bytes_per_launch")
+                key = f"{a.scene}-r{a.resolution}-s{a.samples}-n{world}-{dom}"
+                traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         line = {
@@ -236,12 +252,14 @@ def main():
                        "parallelism": f"image bands x{world} + RCCL all_gather" if world > 1 else "single GPU",
                        "rays_per_frame": total_rays / a.steps,
                        "camera_samples_per_frame": total_samples / a.steps,
-                       "kernel_ms_per_frame": kernel_ms,
-                       "camera_Msamples_per_s": total_samples / elapsed / 1e6},
+                       "gpu_ms_per_frame": render_ms,
+                       "phase_ms_per_frame": {k: v[0] / a.steps for k, v in phases.items()},
+                       "camera_Msamples_per_s": total_samples / elapsed / 1e6,
+                       "algorithm": a.algorithm},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "kernel": "render_kernel<false>"},
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                         "kernel": kernel_names.get(dom, dom), "kernel_ms": dom_ms / dom_launches,
+                         "algorithmic_bytes_per_launch": alg_bytes / dom_launches if alg_bytes else None},
         }
         if world == 1 and a.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(scene_file, a.resolution, a.samples, a.cpu_seconds)

@@ -57,7 +57,16 @@ typedef struct yrt_render_params {
     int band_offset;   /*   (band=1,stride=1,offset=0: contiguous rows) */
     int out_stride;    /* output row stride in pixels; 0 -> tile_w */
     int count_work;    /* 1: also count box/instance/primitive tests (slower; for roofline bytes) */
+    int algorithm;     /* YRT_ALGO_*: identical results, different schedules */
+    int timing;        /* 1: record HIP events per kernel phase (read with yrt_last_timings);
+                          2: keep adding to the previous record (time a loop of renders) */
 } yrt_render_params;
+
+/* render algorithms: identical outputs, different schedules
+ *   WAVEFRONT       kernel per stage, one lane per camera sample, wave-coherent (packet) BVH walk
+ *   MEGAKERNEL      one kernel, one lane per pixel walking the reference's loops
+ *   WAVEFRONT_LANE  kernel per stage, one independent BVH walk per lane */
+enum { YRT_ALGO_WAVEFRONT = 0, YRT_ALGO_MEGAKERNEL = 1, YRT_ALGO_WAVEFRONT_LANE = 2 };
 
 /* counters accumulated by the last yrt_render / yrt_trace_* on a scene handle */
 typedef struct yrt_stats {
@@ -70,7 +79,27 @@ typedef struct yrt_stats {
     unsigned long long prim_tests;
     unsigned long long shaded_hits;
     unsigned long long texture_lookups;
+    unsigned long long shadow_rays;     /* the shadow-ray phase alone (intersect_any calls) */
+    unsigned long long shadow_box_tests;        /* count_work only */
+    unsigned long long shadow_instance_entries; /* count_work only */
+    unsigned long long shadow_prim_tests;       /* count_work only */
 } yrt_stats;
+
+/* GPU time per kernel phase of the last render (HIP events on the launch stream) */
+enum {
+    YRT_PHASE_PRIMARY = 0,    /* camera rays + closest hit + surface */
+    YRT_PHASE_SHADOW = 1,     /* shadow rays (any hit) */
+    YRT_PHASE_SHADE = 2,      /* lighting + mirror-ray compaction */
+    YRT_PHASE_BOUNCE = 3,     /* closest hit of mirror rays */
+    YRT_PHASE_FOLD = 4,       /* reflection fold */
+    YRT_PHASE_ACCUMULATE = 5, /* ordered per-pixel sum */
+    YRT_PHASE_MEGAKERNEL = 6, /* the one-kernel path */
+    YRT_PHASE_COUNT = 8
+};
+typedef struct yrt_timings {
+    float ms[YRT_PHASE_COUNT];
+    int launches[YRT_PHASE_COUNT];
+} yrt_timings;
 
 /* ---- library ---- */
 int yrt_abi_version(void);
@@ -118,6 +147,8 @@ int yrt_trace_first(yrt_scene* ds, const float* rays, int n, unsigned char* hit,
 int yrt_trace_any(yrt_scene* ds, const float* rays, int n, unsigned char* hit, int mem, void* stream);
 /* counters of the last render/trace call on this handle (synchronises the stream) */
 int yrt_last_stats(yrt_scene* ds, yrt_stats* stats);
+/* per-phase GPU times of the last yrt_render with p->timing = 1 (synchronises) */
+int yrt_last_timings(yrt_scene* ds, yrt_timings* timings);
 
 /* ---- image output ---- */
 /* tonemap (src/image.cpp:55-77, exposure 0, srgb) of n RGBA f32 pixels into RGBA8 */

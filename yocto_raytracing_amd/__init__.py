@@ -27,6 +27,7 @@ __all__ = [
     "intersect_any", "tonemap", "save_hdr_or_ldr", "render_params", "device_count", "YrtError",
 ]
 
+ALGORITHMS = {"wavefront": 0, "megakernel": 1, "wavefront_lane": 2}
 INFO_FIELDS = ("cameras", "textures", "materials", "shapes", "instances", "lights",
                "bvh_nodes", "bvh_depth", "shape_bvh_depth", "triangles", "lines", "points")
 
@@ -116,6 +117,13 @@ class DeviceScene:
         check(N.lib.yrt_render(self._h, C.byref(params), C.c_void_p(out_ptr), mem,
                                C.c_void_p(stream or 0)), "yrt_render")
 
+    def last_timings(self) -> dict:
+        """per-phase GPU ms of the last render with timing=True: {phase: (ms, launches)}"""
+        t = N.Timings()
+        check(N.lib.yrt_last_timings(self._h, C.byref(t)), "yrt_last_timings")
+        return {name: (float(t.ms[k]), int(t.launches[k])) for k, name in enumerate(N.PHASES)
+                if t.launches[k]}
+
     def last_stats(self) -> dict:
         s = Stats()
         check(N.lib.yrt_last_stats(self._h, C.byref(s)), "yrt_last_stats")
@@ -143,7 +151,8 @@ def build_bvh(scn: Scene, equal_num: bool = False) -> None:
 
 def render_params(amb=(0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1, *,
                   width: int = 0, max_depth: int = 16, camera: int = 0, window=None,
-                  band=(1, 1, 0), count_work: bool = False) -> RenderParams:
+                  band=(1, 1, 0), count_work: bool = False, algorithm: str = "wavefront",
+                  timing: int = 0) -> RenderParams:
     p = RenderParams()
     N.lib.yrt_render_params_default(C.byref(p))
     if np.isscalar(amb):
@@ -156,6 +165,8 @@ def render_params(amb=(0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1, 
         p.x0, p.y0, p.tile_w, p.tile_h = (int(v) for v in window)
     p.band, p.band_stride, p.band_offset = (int(v) for v in band)
     p.count_work = 1 if count_work else 0
+    p.algorithm = ALGORITHMS[algorithm]
+    p.timing = int(timing)
     return p
 
 
@@ -167,14 +178,14 @@ def _device_scene(scn, device: int = 0) -> DeviceScene:
 
 def raytrace(scn, amb: Sequence[float] = (0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1,
              *, width: int = 0, max_depth: int = 16, camera: int = 0, window=None,
-             count_work: bool = False, return_stats: bool = False):
+             count_work: bool = False, return_stats: bool = False, algorithm: str = "wavefront"):
     """raytrace (src/raytrace.cpp:213): RGBA float32 image (H, W, 4), row-major.
 
     `samples` is per axis (s*s samples per pixel), `resolution` the vertical size.
     `window` = (x0, y0, w, h) renders a sub-rectangle only."""
     ds = _device_scene(scn)
     p = render_params(amb, resolution, samples, width=width, max_depth=max_depth, camera=camera,
-                      window=window, count_work=count_work)
+                      window=window, count_work=count_work, algorithm=algorithm)
     W, H = ds.image_size(p)
     if window is None:
         w, h = W, H

@@ -14,7 +14,7 @@ LIB_PATH = Path(os.environ.get("YRT_LIB", _PKG / "libyrt.so"))
 
 if not LIB_PATH.exists():
     raise ImportError(
-        f"{LIB_PATH} not found: build it with `python -m yocto_raytracing_amd.build` "
+        f"{LIB_PATH} not found: build it with `python yocto_raytracing_amd/build.py` "
         "(or __graft_entry__.build()); there is no fallback path")
 
 lib = C.CDLL(str(LIB_PATH))
@@ -41,13 +41,23 @@ class RenderParams(C.Structure):
         ("band_offset", C.c_int),
         ("out_stride", C.c_int),
         ("count_work", C.c_int),
+        ("algorithm", C.c_int),
+        ("timing", C.c_int),
     ]
 
 
 class Stats(C.Structure):
     _fields_ = [(n, C.c_ulonglong) for n in (
         "rays", "camera_samples", "depth_truncated", "stack_overflow", "box_tests",
-        "instance_entries", "prim_tests", "shaded_hits", "texture_lookups")]
+        "instance_entries", "prim_tests", "shaded_hits", "texture_lookups", "shadow_rays",
+        "shadow_box_tests", "shadow_instance_entries", "shadow_prim_tests")]
+
+
+PHASES = ("primary", "shadow", "shade", "bounce", "fold", "accumulate", "megakernel", "unused")
+
+
+class Timings(C.Structure):
+    _fields_ = [("ms", C.c_float * 8), ("launches", C.c_int * 8)]
 
 
 _vp = C.c_void_p
@@ -72,13 +82,17 @@ _sig = {
     "yrt_trace_first": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp]),
     "yrt_trace_any": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int, _vp]),
     "yrt_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
+    "yrt_last_timings": (C.c_int, [_vp, C.POINTER(Timings)]),
     "yrt_tonemap": (C.c_int, [_vp, C.c_int, _vp, C.c_int, _vp]),
     "yrt_save_image": (C.c_int, [C.c_char_p, _vp, C.c_int, C.c_int]),
 }
 EXPORTS = tuple(_sig)
 
 for _name, (_res, _args) in _sig.items():
-    _f = getattr(lib, _name)
+    try:
+        _f = getattr(lib, _name)
+    except AttributeError as e:
+        raise ImportError(f"{LIB_PATH} is stale (missing {_name}): rebuild it") from e
     _f.restype = _res
     _f.argtypes = _args
 

@@ -5,8 +5,8 @@ with -ffp-contract=off so that no a*b+c is fused anywhere on the hot path (the
 reference's x86-64 build has no FMA). Objects are rebuilt only when
 a source or header is newer.
 
-    python -m yocto_raytracing_amd.build            # library + CLI
-    python -m yocto_raytracing_amd.build --oracle   # + oracle/liboracle.so (+ oracle/_ref if present)
+    python yocto_raytracing_amd/build.py            # library + CLI
+    python yocto_raytracing_amd/build.py --oracle   # + oracle/liboracle.so (+ oracle/_ref if present)
 """
 from __future__ import annotations
 
@@ -27,7 +27,7 @@ CLANGXX = os.environ.get("YRT_CXX", "/opt/rocm/lib/llvm/bin/clang++")
 ARCH = os.environ.get("YRT_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["obj_loader.cpp", "png.cpp", "scene_io.cpp", "bvh_build.cpp",
-           "device_scene.cpp", "capi.cpp", "render.hip"]
+           "device_scene.cpp", "capi.cpp", "render.hip", "wavefront.hip"]
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           f"-I{CSRC}", f"-I{ROOT / 'include'}"]
 

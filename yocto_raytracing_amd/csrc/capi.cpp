@@ -295,7 +295,16 @@ int yrt_render(yrt_scene* s, const yrt_render_params* p, float* out, int mem, vo
         size_t bytes = (size_t)a.out_stride * r.th * 4 * sizeof(float);
         void* dst = mem == YRT_MEM_DEVICE ? (void*)out : scratch(s, bytes);
         hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
-        hip_check(yrt::launch_render(*s->ds, a, dst, s->counters, p->count_work != 0, st), "render kernel launch");
+        // timing 1: start a new record; 2: keep accumulating across calls (bench loops)
+        if (!(p->timing == 2 && s->ds->timer.on)) s->ds->timer.reset(p->timing != 0);
+        if (p->algorithm == YRT_ALGO_MEGAKERNEL)
+            hip_check(yrt::launch_render(*s->ds, a, dst, s->counters, p->count_work != 0, st), "render kernel launch");
+        else if (p->algorithm == YRT_ALGO_WAVEFRONT || p->algorithm == YRT_ALGO_WAVEFRONT_LANE)
+            hip_check(yrt::launch_render_wavefront(*s->ds, a, dst, s->counters, p->count_work != 0,
+                                                   p->algorithm == YRT_ALGO_WAVEFRONT, st),
+                      "wavefront render launch");
+        else
+            throw std::invalid_argument("unknown algorithm");
         s->last_stream = st;
         if (mem != YRT_MEM_DEVICE) {
             hip_check(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
@@ -367,6 +376,19 @@ int yrt_last_stats(yrt_scene* s, yrt_stats* out) {
         out->prim_tests = c[yrt::cnt_prim_tests];
         out->shaded_hits = c[yrt::cnt_shaded_hits];
         out->texture_lookups = c[yrt::cnt_tex_lookups];
+        out->shadow_rays = c[yrt::cnt_shadow_rays];
+        out->shadow_box_tests = c[yrt::cnt_shadow_box_tests];
+        out->shadow_instance_entries = c[yrt::cnt_shadow_inst_entries];
+        out->shadow_prim_tests = c[yrt::cnt_shadow_prim_tests];
+        return YRT_OK;
+    });
+}
+
+int yrt_last_timings(yrt_scene* s, yrt_timings* out) {
+    if (!s || !out) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        hip_check(hipSetDevice(s->ds->device), "hipSetDevice");
+        s->ds->timer.collect(out->ms, out->launches);
         return YRT_OK;
     });
 }

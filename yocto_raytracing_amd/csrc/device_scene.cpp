@@ -84,16 +84,28 @@ device_scene* device_scene_create(const scene& scn, int device) {
     if (scn.cameras.empty()) throw std::runtime_error("scene has no camera");
     if (scn.instances.empty()) throw std::runtime_error("scene has no instances");
 
+    // the kernels test an inner node's two children together (records start, start+1),
+    // as make_node always builds them (scene.cpp:595-601)
+    auto binary = [](const bvh_tree& t) {
+        for (auto& n : t.nodes)
+            if (!n.isleaf && n.count != 2) return false;
+        return !t.nodes.empty();
+    };
+    if (!binary(scn.bvh)) throw std::runtime_error("instance BVH is not binary (unsupported)");
+    for (auto& s : scn.shapes)
+        if (!binary(s.bvh)) throw std::runtime_error("shape BVH of " + s.name + " is not binary (unsupported)");
+
     auto ds = new device_scene();
     ds->device = device;
     ds->cameras = scn.cameras;
     ds->top_depth = bvh_max_depth(scn.bvh);
     for (auto& s : scn.shapes) ds->shape_depth = std::max(ds->shape_depth, bvh_max_depth(s.bvh));
-    if (ds->top_depth > top_stack_cap || ds->shape_depth > shape_stack_cap) {
+    if (ds->top_depth + ds->shape_depth > traversal_stack_cap) {
         int td = ds->top_depth, sd = ds->shape_depth;
         delete ds;
         throw std::runtime_error("BVH too deep for the kernel stacks (instance " + std::to_string(td) +
-                                 ", shape " + std::to_string(sd) + ")");
+                                 " + shape " + std::to_string(sd) + " > " +
+                                 std::to_string(traversal_stack_cap) + ")");
     }
 
     // ---- shapes: nodes, leaf-ordered primitives, elements, vertices ----
@@ -114,7 +126,9 @@ device_scene* device_scene_create(const scene& scn, int device) {
         int elem_base = (int)elems.size();
         int vert_base = (int)vpos.size();
         for (auto& n : s.bvh.nodes) {
-            uint32_t start = n.isleaf ? n.start + prim_base : n.start + node_base;
+            // leaves: absolute primitive slot; inner nodes: child index relative to the
+            // shape's root (the traversal keeps shape-level stack entries root-relative)
+            uint32_t start = n.isleaf ? n.start + prim_base : n.start;
             snodes.push_back(node_lo(n, start));
             snodes.push_back(node_hi(n));
         }
@@ -154,6 +168,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
             vuv.push_back({t.x, t.y});
         }
         shapes.push_back({node_base, kind, elem_base, vert_base});
+        ds->max_shape_nodes = std::max(ds->max_shape_nodes, s.bvh.nodes.size());
     }
 
     // ---- instance level: nodes + instances permuted into leaf order ----
@@ -179,6 +194,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
         float rs = m.rs;
         float ns = (rs) ? 2 / std::pow(rs, 4.0f) - 2 : 1e6f;  // raytrace.cpp:144
         int flags = (m.kr.x > 0.0f || m.kr.y > 0.0f || m.kr.z > 0.0f) ? mat_reflective : 0;
+        if (flags & mat_reflective) ds->reflective = true;
         for (int t : {m.kd_txt, m.ks_txt}) {
             if (t >= (int)scn.textures.size() || (t >= 0 && scn.textures[t].pixels.empty()))
                 throw std::runtime_error("material " + m.name + " references a missing texture");
@@ -262,20 +278,65 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.texinfo = (const i4*)(base + o_texinfo);
     v.srgb = (const float*)(base + o_srgb);
     v.nlights = (int)lights.size() / 6;
+    ds->nlights = v.nlights;
     v.ntnodes = (int)tnodes.size() / 2;
     ds->ntnodes = tnodes.size() / 2;
+    ds->narrow_stack = ds->ntnodes < 65536 && ds->max_shape_nodes < 65536;
     ds->nsnodes = snodes.size() / 2;
     ds->nsprims = sprims.size() / 3;
     ds->ninst = tinst.size() / 4;
     return ds;
 }
 
+int phase_timer::begin(int phase, hipStream_t s) {
+    if (!on) return -1;
+    if (used >= phase_of.size()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess) return -1;
+        if (hipEventCreate(&b) != hipSuccess) {
+            hipEventDestroy(a);
+            return -1;
+        }
+        pool.push_back(a);
+        pool.push_back(b);
+        phase_of.push_back(0);
+    }
+    int idx = (int)used++;
+    phase_of[idx] = phase;
+    hipEventRecord(pool[2 * idx], s);
+    return idx;
+}
+
+void phase_timer::end(int idx, hipStream_t s) {
+    if (idx >= 0) hipEventRecord(pool[2 * idx + 1], s);
+}
+
+void phase_timer::collect(float* ms, int* launches) {
+    for (int p = 0; p < phase_count; p++) {
+        ms[p] = 0;
+        launches[p] = 0;
+    }
+    for (size_t i = 0; i < used; i++) {
+        float t = 0;
+        hipEventSynchronize(pool[2 * i + 1]);
+        if (hipEventElapsedTime(&t, pool[2 * i], pool[2 * i + 1]) == hipSuccess) ms[phase_of[i]] += t;
+        launches[phase_of[i]]++;
+    }
+}
+
+void phase_timer::destroy() {
+    for (auto e : pool) hipEventDestroy(e);
+    pool.clear();
+    phase_of.clear();
+    used = 0;
+}
+
 void device_scene_destroy(device_scene* ds) {
     if (!ds) return;
-    if (ds->arena) {
-        hipSetDevice(ds->device);
-        hipFree(ds->arena);
-    }
+    hipSetDevice(ds->device);
+    ds->timer.destroy();
+    if (ds->arena) hipFree(ds->arena);
+    if (ds->work) hipFree(ds->work);
     delete ds;
 }
 

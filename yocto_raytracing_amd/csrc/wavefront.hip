@@ -1,0 +1,551 @@
+// wavefront.hip -- the default render path: raytrace() (src/raytrace.cpp:213-254)
+// as a wavefront pipeline of small gfx950 kernels over one lane per CAMERA SAMPLE.
+//
+// Per chunk of camera samples (a whole 1080p x 64 spp frame is one chunk; the
+// per-sample state, ~70 B, lives in HBM -- 9 GB at c4 -- rather than in registers):
+//   k_primary   eval_camera (:6-37) + closest hit (intersect_first, scene.cpp:483)
+//               + eval_pos/eval_norm/eval_texcoord (scene.h:159-218) -> surface SoA
+//   k_shadow    per light: the shadow ray of shade() (raytrace.cpp:129-133),
+//               intersect_any (scene.cpp:489) -> occlusion byte
+//   k_shade     the rest of shade() (:99-206): ambient, textures, Blinn-Phong or
+//               lines lighting per unoccluded light, and for reflective hits the
+//               mirror ray, compacted into the next level with one ballot + one
+//               atomic per wave
+//   (levels 1..max_depth-1: k_bounce (closest hit of the compacted rays), k_shadow,
+//    k_shade; then k_fold back to front: R_k = (D_k + R_{k+1}*kr_k) + la_k)
+//   k_accumulate  the ordered per-pixel sum of raytrace.cpp:232-249
+//
+// Why: every traversal kernel carries only its ray and stack (few VGPRs, high
+// occupancy), lanes of one wave are 64 samples of one pixel (s=8) or an 8x8 pixel
+// tile (s=1), so their rays are nearly identical and stay converged through both
+// BVH levels, and shadow rays of one light are traced together.
+//
+// Parity: each sample's arithmetic is shade()'s, in its order (trace_common.h);
+// samples are summed per pixel in the reference's jj-major / ii-minor order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "packet_trace.h"
+#include "trace_common.h"
+#include "yrt_render.h"
+
+namespace yrt {
+namespace {
+
+constexpr int WF_BLOCK = 256;
+constexpr int MAX_LEVELS = 16;
+constexpr int TILE = 8;  // pixel tiles of 8x8 in the sample enumeration
+
+struct wf_buffers {
+    f4* surf0;          // {p.xyz, info}: info = mat*4+kind, -1 miss, -2 not a sample
+    f4* surf1;          // {n.xyz, u}
+    float* surfv;       // v
+    unsigned char* occl;  // [light][sample]
+    f4* rad;            // level-0 radiance per sample
+    // bounce levels (reflective scenes only)
+    f4* ray_o[MAX_LEVELS];  // level k >= 1: {o.xyz, parent index}
+    f4* ray_d[MAX_LEVELS];  // level k >= 1: {d.xyz, -}
+    f4* R[MAX_LEVELS];      // level k >= 1 radiance (level 0 uses rad)
+    f4* rec0[MAX_LEVELS];   // level k: {D.xyz, child index}
+    f4* rec1[MAX_LEVELS];   // {la.xyz, -}
+    f4* rec2[MAX_LEVELS];   // {kr.xyz, -}
+    int* count;             // count[k]: rays at level k (k >= 1)
+    int capacity;           // samples per chunk
+    int nlevels;            // levels allocated
+};
+
+struct chunk_args {
+    long long pix0;  // first pixel (in tile enumeration order) of this chunk
+    int npix;        // pixels in this chunk
+    int spp;
+    int tiles_x;     // 8x8 tiles across the window
+};
+
+// pixel enumeration: 8x8 tiles across the local window, row-major tiles, row-major
+// pixels inside a tile; samples of a pixel consecutive in jj-major / ii-minor order
+__device__ __forceinline__ bool pixel_of(const dev_render_args& A, int tiles_x, long long p, int& lx, int& ly,
+                                         int& i, int& j) {
+    long long t = p / (TILE * TILE);
+    int w = (int)(p % (TILE * TILE));
+    lx = (int)(t % tiles_x) * TILE + (w % TILE);
+    ly = (int)(t / tiles_x) * TILE + (w / TILE);
+    if (lx >= A.tile_w || ly >= A.tile_h) return false;
+    i = A.x0 + lx;
+    int b = ly / A.band, r = ly % A.band;
+    j = A.y0 + (b * A.band_stride + A.band_offset) * A.band + r;
+    return i < A.width && j < A.height;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush(unsigned long long* counters, int idx, unsigned long long v) {
+    unsigned long long s = wave_sum(v);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(counters + idx, s);
+}
+
+__device__ __forceinline__ void flush_work(unsigned long long* counters, const work_counts& wc) {
+    flush<true>(counters, cnt_box_tests, wc.box);
+    flush<true>(counters, cnt_inst_entries, wc.inst);
+    flush<true>(counters, cnt_prim_tests, wc.prim);
+    flush<true>(counters, cnt_shaded_hits, wc.hits);
+    flush<true>(counters, cnt_tex_lookups, wc.tex);
+}
+
+__device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool hit, const surface& sf) {
+    if (!hit) {
+        B.surf0[idx] = {0, 0, 0, __int_as_float(-1)};
+        return;
+    }
+    B.surf0[idx] = {sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind)};
+    B.surf1[idx] = {sf.n.x, sf.n.y, sf.n.z, sf.uv.x};
+    B.surfv[idx] = sf.uv.y;
+}
+
+// the two traversal schedules behind one call: PACKET = wave-coherent walk
+// (packet_trace.h, default), otherwise one independent walk per lane
+// (trace_common.h). Both are called in wave-uniform control flow.
+template <bool ANY, bool COUNT, bool PACKET, typename SE>
+struct tracer {
+    static constexpr int WAVES = WF_BLOCK / 64;
+    SE* lane_stk;
+    wave_stack wst;
+    __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
+                                          work_counts& wc) {
+        if (PACKET) return packet_trace<ANY, COUNT>(S, ray, valid, hr, wst, wc);
+        if (!valid) return false;
+        if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
+        return traverse<false, COUNT, WF_BLOCK>(S, ray, hr, lane_stk, wc);
+    }
+};
+
+// LDS for either schedule: per-lane columns, or one {node, mask} stack per wave
+template <bool PACKET, typename SE>
+struct traversal_lds;
+template <typename SE>
+struct traversal_lds<false, SE> {
+    SE lane[traversal_stack_cap * WF_BLOCK];
+};
+template <typename SE>
+struct traversal_lds<true, SE> {
+    unsigned long long mask[WF_BLOCK / 64][traversal_stack_cap];
+    int node[WF_BLOCK / 64][traversal_stack_cap];
+};
+
+template <bool ANY, bool COUNT, bool PACKET, typename SE>
+__device__ __forceinline__ tracer<ANY, COUNT, PACKET, SE> make_tracer(traversal_lds<PACKET, SE>& L) {
+    tracer<ANY, COUNT, PACKET, SE> t;
+    if constexpr (PACKET) {
+        const int w = threadIdx.x / 64;
+        t.lane_stk = nullptr;
+        t.wst = {L.node[w], L.mask[w]};
+    } else {
+        t.lane_stk = L.lane + threadIdx.x;
+        t.wst = {nullptr, nullptr};
+    }
+    return t;
+}
+
+// ---- level 0: camera rays + closest hit + surface ----
+template <bool COUNT, bool PACKET, typename SE>
+__global__ __launch_bounds__(WF_BLOCK) void k_primary(dev_scene_view S, dev_render_args A, chunk_args C,
+                                                      wf_buffers B, unsigned long long* counters) {
+    __shared__ traversal_lds<PACKET, SE> lds;
+    auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
+    const int idx = blockIdx.x * WF_BLOCK + threadIdx.x;
+    const int nsamp = C.npix * C.spp;
+    work_counts wc;
+    bool valid = false;
+    ray3 ray = {{0, 0, 0}, {0, 0, 1}, ray_eps, flt_max};
+    if (idx < nsamp) {
+        const long long p = C.pix0 + idx / C.spp;
+        const int q = idx % C.spp;
+        int lx, ly, i, j;
+        valid = pixel_of(A, C.tiles_x, p, lx, ly, i, j);
+        if (valid) {
+            const int ns = A.samples;
+            ray = camera_ray(A.cam, A.width, A.height, ns, i, j, q % ns, q / ns);
+        } else {
+            B.surf0[idx] = {0, 0, 0, __int_as_float(-2)};
+        }
+    }
+    hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
+    const bool hit = T.trace(S, ray, valid, hr, wc);
+    if (valid) {
+        surface sf = {};
+        if (hit) {
+            sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
+            if (COUNT) wc.hits++;
+        }
+        store_surface(B, idx, hit, sf);
+    }
+    flush<false>(counters, cnt_rays, valid ? 1 : 0);
+    flush<false>(counters, cnt_samples, valid ? 1 : 0);
+    if (COUNT) flush_work(counters, wc);
+}
+
+// ---- levels >= 1: closest hit of the compacted mirror rays (grid-stride) ----
+template <bool COUNT, bool PACKET, typename SE>
+__global__ __launch_bounds__(WF_BLOCK) void k_bounce(dev_scene_view S, int level, wf_buffers B,
+                                                     unsigned long long* counters) {
+    __shared__ traversal_lds<PACKET, SE> lds;
+    auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
+    const int n = B.count[level];
+    work_counts wc;
+    unsigned long long rays = 0;
+    const int stride = gridDim.x * WF_BLOCK;
+    const int nround = (n + stride - 1) / stride;  // uniform: every lane reaches the traversal
+    for (int round = 0; round < nround; round++) {
+        const int idx = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
+        const bool valid = idx < n;
+        ray3 ray = {{0, 0, 0}, {0, 0, 1}, ray_eps, flt_max};
+        if (valid) {
+            float4 o = ld4(B.ray_o[level] + idx), d = ld4(B.ray_d[level] + idx);
+            ray = {xyz(o), xyz(d), ray_eps, flt_max};
+            rays++;
+        }
+        hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
+        const bool hit = T.trace(S, ray, valid, hr, wc);
+        if (valid) {
+            surface sf = {};
+            if (hit) {
+                sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
+                if (COUNT) wc.hits++;
+            }
+            store_surface(B, idx, hit, sf);
+        }
+    }
+    flush<false>(counters, cnt_rays, rays);
+    if (COUNT) flush_work(counters, wc);
+}
+
+// ---- shadow rays (raytrace.cpp:128-133): one light per blockIdx.y ----
+template <bool COUNT, bool PACKET, typename SE>
+__global__ __launch_bounds__(WF_BLOCK) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
+                                                     unsigned long long* counters) {
+    __shared__ traversal_lds<PACKET, SE> lds;
+    auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
+    const int n = level ? B.count[level] : nsamp_level0;
+    const int li = blockIdx.y;
+    const f4* lr = S.lights + 6 * li;
+    const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
+    const vec3f lp0 = xyz(ld4(lr + 4));
+    work_counts wc;
+    unsigned long long rays = 0;
+    const int stride = gridDim.x * WF_BLOCK;
+    const int nround = (n + stride - 1) / stride;
+    for (int round = 0; round < nround; round++) {
+        const int idx = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
+        bool valid = false;
+        ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
+        if (idx < n) {
+            float4 s0 = ld4(B.surf0 + idx);
+            if (ibits(s0.w) >= 0) {
+                vec3f p = xyz(s0);
+                vec3f tp = transform_point(lf, lp0 - p);
+                vec3f l = normalize(tp);
+                float r = length(tp);
+                sr = {p, l, 0.01f, r - 0.01f};
+                valid = true;
+                rays++;
+            }
+        }
+        hit_record hr;
+        const bool occ = T.trace(S, sr, valid, hr, wc);
+        if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
+    }
+    flush<false>(counters, cnt_rays, rays);
+    flush<false>(counters, cnt_shadow_rays, rays);
+    if (COUNT) {
+        flush_work(counters, wc);
+        flush<true>(counters, cnt_shadow_box_tests, wc.box);
+        flush<true>(counters, cnt_shadow_inst_entries, wc.inst);
+        flush<true>(counters, cnt_shadow_prim_tests, wc.prim);
+    }
+}
+
+// ---- shade() after the queries (raytrace.cpp:99-206) ----
+template <bool COUNT>
+__global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
+                                                    int max_depth, wf_buffers B, unsigned long long* counters) {
+    const int n = level ? B.count[level] : nsamp_level0;
+    work_counts wc;
+    unsigned long long truncated = 0;
+    const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
+    const vec3f cam_o = {A.cam.ox, A.cam.oy, A.cam.oz};
+    // the loop bound is uniform per wave so every lane reaches the ballot below
+    const int stride = gridDim.x * WF_BLOCK;
+    const int nround = (n + stride - 1) / stride;
+    for (int round = 0; round < nround; round++) {
+        const int idx = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
+        bool spawn = false;
+        vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0}, rec_kr = {0, 0, 0};
+        if (idx < n) {
+            float4 s0 = ld4(B.surf0 + idx);
+            const int info = ibits(s0.w);
+            vec3f R = {0, 0, 0};
+            bool write_r = info != -2;
+            if (info >= 0) {
+                float4 s1 = ld4(B.surf1 + idx);
+                p = xyz(s0);
+                const vec3f nrm = xyz(s1);
+                const vec2f uv = {s1.w, B.surfv[idx]};
+                const int mat = info >> 2, kind = info & 3;
+                const vec3f ro = level ? xyz(ld4(B.ray_o[level] + idx)) : cam_o;
+                float4 m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1);
+                float4 m2 = ld4(S.mats + 4 * mat + 2), m3 = ld4(S.mats + 4 * mat + 3);
+                const vec3f kd0 = xyz(m0), ks0 = xyz(m1), kr = xyz(m2);
+                const float ns = m0.w;
+                const int kd_txt = ibits(m1.w), ks_txt = ibits(m2.w);
+                const bool reflective = ibits(m3.w) & mat_reflective;
+                vec3f la = amb * kd0;
+                vec3f tkd = {1, 1, 1}, tks = {1, 1, 1};
+                if (kd_txt >= 0) {
+                    tkd = eval_texture<COUNT>(S, kd_txt, uv, wc);
+                    la = la * tkd;
+                }
+                if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, uv, wc);
+                vec3f c = {0.0f, 0.0f, 0.0f};
+                for (int li = 0; li < S.nlights; li++) {
+                    if (B.occl[(size_t)li * B.capacity + idx]) continue;
+                    const f4* lr = S.lights + 6 * li;
+                    frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
+                    vec3f lp0 = xyz(ld4(lr + 4)), ke = xyz(ld4(lr + 5));
+                    vec3f tp = transform_point(lf, lp0 - p);
+                    vec3f l = normalize(tp);
+                    float r = length(tp);
+                    vec3f v = normalize(ro - p);
+                    vec3f h = normalize(v + l);
+                    vec3f kd = kd0, ks = ks0;
+                    if (kd_txt >= 0) kd = kd * tkd;
+                    if (ks_txt >= 0) ks = ks * tks;
+                    vec3f ld = kd * (ke / (r * r));
+                    vec3f ls = ks * (ke / (r * r));
+                    if (kind == kind_lines) {
+                        float prodnl = dot(nrm, l);
+                        float prodnh = dot(nrm, h);
+                        if (prodnl < 0.0f) prodnl *= -1;
+                        if (prodnh < 0.0f) prodnh *= -1;
+                        float sinnl = __builtin_sqrtf(1.0f - prodnl);
+                        float sinnh = __builtin_sqrtf(1.0f - prodnh);
+                        ld = ld * sinnl;
+                        ls = ls * powf_cr(sinnh, ns);
+                    } else {
+                        ld = ld * smax(0.0f, dot(nrm, l));
+                        ls = ls * powf_cr(smax(0.0f, dot(nrm, h)), ns);
+                    }
+                    c = c + (ld + ls);
+                }
+                if (!reflective) {
+                    R = c + la;
+                } else if (level + 1 >= max_depth || level + 1 >= B.nlevels) {
+                    // depth cap: the reflected contribution counts as a miss (col = 0)
+                    truncated++;
+                    vec3f t = {0.0f * kr.x, 0.0f * kr.y, 0.0f * kr.z};
+                    R = (c + t) + la;
+                } else {
+                    spawn = true;
+                    vec3f v = normalize(ro - p);
+                    dr = (nrm * 2.0f * dot(nrm, v)) - v;
+                    rec_d = c;
+                    rec_la = la;
+                    rec_kr = kr;
+                    write_r = false;
+                }
+                if (COUNT) wc.hits++;
+            }
+            if (write_r) {
+                f4* dst = level ? B.R[level] : B.rad;
+                dst[idx] = {R.x, R.y, R.z, 1.0f};
+            }
+        }
+        // wave compaction of the mirror rays: one atomic per wave, lanes take
+        // consecutive slots in lane order
+        const unsigned long long mask = __ballot(spawn);
+        if (mask) {
+            int base = 0;
+            const int lane = threadIdx.x & 63;
+            const int first = __ffsll((long long)mask) - 1;
+            if (lane == first) base = atomicAdd(B.count + level + 1, __popcll(mask));
+            base = __shfl(base, first, 64);
+            if (spawn) {
+                const int slot = base + __popcll(mask & ((1ull << lane) - 1));
+                B.ray_o[level + 1][slot] = {p.x, p.y, p.z, __int_as_float(idx)};
+                B.ray_d[level + 1][slot] = {dr.x, dr.y, dr.z, 0};
+                B.rec0[level][idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
+                B.rec1[level][idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
+                B.rec2[level][idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
+            }
+        }
+    }
+    flush<false>(counters, cnt_depth_truncated, truncated);
+    if (COUNT) flush_work(counters, wc);
+}
+
+// ---- fold level k+1 back onto its mirror samples at level k (raytrace.cpp:201-206):
+// R_k = (D_k + R_{k+1}*kr_k) + la_k, one lane per child ray (its parent is ray_o.w) ----
+__global__ __launch_bounds__(WF_BLOCK) void k_fold_children(int level, wf_buffers B) {
+    // one lane per CHILD ray at level+1: its parent sample is ray_o.w
+    const int n = B.count[level + 1];
+    f4* dst_base = level ? B.R[level] : B.rad;
+    for (int c = blockIdx.x * WF_BLOCK + threadIdx.x; c < n; c += gridDim.x * WF_BLOCK) {
+        const int parent = ibits(B.ray_o[level + 1][c].w);
+        float4 r = ld4(B.R[level + 1] + c);
+        float4 d = ld4(B.rec0[level] + parent), la = ld4(B.rec1[level] + parent), kr = ld4(B.rec2[level] + parent);
+        vec3f col = {r.x, r.y, r.z};
+        vec3f cc = {d.x, d.y, d.z};
+        cc = cc + vec3f{col.x * kr.x, col.y * kr.y, col.z * kr.z};
+        cc = cc + xyz(la);
+        dst_base[parent] = {cc.x, cc.y, cc.z, 1.0f};
+    }
+}
+
+// ---- ordered per-pixel sum (raytrace.cpp:232-249) ----
+__global__ __launch_bounds__(WF_BLOCK) void k_accumulate(dev_render_args A, chunk_args C, wf_buffers B,
+                                                         float4* __restrict__ out) {
+    const int pl = blockIdx.x * WF_BLOCK + threadIdx.x;
+    if (pl >= C.npix) return;
+    int lx, ly, i, j;
+    const long long p = C.pix0 + pl;
+    bool valid = pixel_of(A, C.tiles_x, p, lx, ly, i, j);
+    if (lx >= A.tile_w || ly >= A.tile_h) return;
+    if (!valid) {
+        out[(size_t)ly * A.out_stride + lx] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        return;
+    }
+    vec4f acc = {0, 0, 0, 0};
+    const f4* r = B.rad + (size_t)pl * C.spp;
+    for (int q = 0; q < C.spp; q++) {
+        float4 c = ld4(r + q);
+        acc = {acc.x + c.x, acc.y + c.y, acc.z + c.z, acc.w + 1.0f};
+    }
+    const float d = float(C.spp);
+    out[(size_t)ly * A.out_stride + lx] = make_float4(acc.x / d, acc.y / d, acc.z / d, 1.0f);
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+size_t workspace_bytes(int cap, int nlights, int nlevels) {
+    size_t c = (size_t)cap;
+    size_t b = align_up(sizeof(int) * (MAX_LEVELS + 1));
+    b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
+    if (nlevels > 1) b += (size_t)(nlevels - 1) * 3 * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
+    return b;
+}
+
+wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
+    wf_buffers B = {};
+    char* p = (char*)base;
+    size_t c = (size_t)cap;
+    auto take = [&](size_t bytes) {
+        char* q = p;
+        p += align_up(bytes);
+        return (void*)q;
+    };
+    B.count = (int*)take(sizeof(int) * (MAX_LEVELS + 1));
+    B.surf0 = (f4*)take(16 * c);
+    B.surf1 = (f4*)take(16 * c);
+    B.surfv = (float*)take(4 * c);
+    B.occl = (unsigned char*)take(c * std::max(nlights, 1));
+    B.rad = (f4*)take(16 * c);
+    for (int k = 1; k < nlevels; k++) {
+        B.ray_o[k] = (f4*)take(16 * c);
+        B.ray_d[k] = (f4*)take(16 * c);
+        B.R[k] = (f4*)take(16 * c);
+    }
+    for (int k = 0; k + 1 < nlevels; k++) {
+        B.rec0[k] = (f4*)take(16 * c);
+        B.rec1[k] = (f4*)take(16 * c);
+        B.rec2[k] = (f4*)take(16 * c);
+    }
+    B.capacity = cap;
+    B.nlevels = nlevels;
+    return B;
+}
+
+template <bool COUNT, bool PACKET, typename SE>
+hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned long long* counters,
+               hipStream_t stream) {
+    const int spp = A.samples * A.samples;
+    const int tiles_x = (A.tile_w + TILE - 1) / TILE;
+    const int tiles_y = (A.tile_h + TILE - 1) / TILE;
+    const long long npix_total = (long long)tiles_x * tiles_y * TILE * TILE;
+    const int nlevels = ds.reflective ? std::min(std::max(A.max_depth, 1), MAX_LEVELS) : 1;
+    const long long target = ds.reflective ? (1ll << 23) : (1ll << 27);
+    int pix_per_chunk = (int)std::max<long long>(1, std::min<long long>(npix_total, target / spp));
+    pix_per_chunk = ((pix_per_chunk + TILE * TILE - 1) / (TILE * TILE)) * TILE * TILE;
+    const int cap = pix_per_chunk * spp;
+    const size_t need = workspace_bytes(cap, ds.nlights, nlevels);
+    if (need > ds.work_bytes) {
+        if (ds.work) hipFree(ds.work);
+        ds.work = nullptr;
+        ds.work_bytes = 0;
+        hipError_t e = hipMalloc(&ds.work, need);
+        if (e != hipSuccess) return e;
+        ds.work_bytes = need;
+    }
+    wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
+    phase_timer& T = ds.timer;
+    const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
+    for (long long pix0 = 0; pix0 < npix_total; pix0 += pix_per_chunk) {
+        chunk_args C = {pix0, (int)std::min<long long>(pix_per_chunk, npix_total - pix0), spp, tiles_x};
+        const int nsamp = C.npix * spp;
+        const int grid = (nsamp + WF_BLOCK - 1) / WF_BLOCK;
+        if (nlevels > 1) {
+            hipError_t e = hipMemsetAsync(B.count, 0, sizeof(int) * (MAX_LEVELS + 1), stream);
+            if (e != hipSuccess) return e;
+        }
+        int t = T.begin(phase_primary, stream);
+        hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, C, B, counters);
+        T.end(t, stream);
+        for (int level = 0; level < nlevels; level++) {
+            if (level > 0) {
+                t = T.begin(phase_bounce, stream);
+                hipLaunchKernelGGL((k_bounce<COUNT, PACKET, SE>), dim3(stride_grid), dim3(WF_BLOCK), 0, stream, ds.view,
+                                   level, B, counters);
+                T.end(t, stream);
+            }
+            if (ds.nlights > 0) {
+                dim3 sg(level ? stride_grid : grid, ds.nlights);
+                t = T.begin(phase_shadow, stream);
+                hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE>), sg, dim3(WF_BLOCK), 0, stream, ds.view, level, nsamp, B,
+                                   counters);
+                T.end(t, stream);
+            }
+            t = T.begin(phase_shade, stream);
+            hipLaunchKernelGGL((k_shade<COUNT>), dim3(level ? stride_grid : grid), dim3(WF_BLOCK), 0, stream, ds.view,
+                               A, level, nsamp, A.max_depth, B, counters);
+            T.end(t, stream);
+        }
+        for (int level = nlevels - 2; level >= 0; level--) {
+            t = T.begin(phase_fold, stream);
+            hipLaunchKernelGGL(k_fold_children, dim3(stride_grid), dim3(WF_BLOCK), 0, stream, level, B);
+            T.end(t, stream);
+        }
+        t = T.begin(phase_accumulate, stream);
+        hipLaunchKernelGGL(k_accumulate, dim3((C.npix + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream, A, C,
+                           B, out);
+        T.end(t, stream);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_render_wavefront(device_scene& ds, const dev_render_args& args, void* out_rgba,
+                                   unsigned long long* counters, bool count_work, bool packet, hipStream_t stream) {
+    if (args.tile_w <= 0 || args.tile_h <= 0) return hipSuccess;
+    float4* out = (float4*)out_rgba;
+    if (packet) {
+        // the per-wave stack holds 32-bit node indices: no narrow/wide split needed
+        return count_work ? run<true, true, uint32_t>(ds, args, out, counters, stream)
+                          : run<false, true, uint32_t>(ds, args, out, counters, stream);
+    }
+    if (ds.narrow_stack)
+        return count_work ? run<true, false, uint16_t>(ds, args, out, counters, stream)
+                          : run<false, false, uint16_t>(ds, args, out, counters, stream);
+    return count_work ? run<true, false, uint32_t>(ds, args, out, counters, stream)
+                      : run<false, false, uint32_t>(ds, args, out, counters, stream);
+}
+
+}  // namespace yrt

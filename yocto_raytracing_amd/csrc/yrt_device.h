@@ -91,6 +91,11 @@ enum counter_index {
     cnt_prim_tests = 6,
     cnt_shaded_hits = 7,
     cnt_tex_lookups = 8,
+    // the shadow-ray phase alone (k_shadow), for its own roofline
+    cnt_shadow_rays = 9,
+    cnt_shadow_box_tests = 10,
+    cnt_shadow_inst_entries = 11,
+    cnt_shadow_prim_tests = 12,
     cnt_count = 16
 };
 

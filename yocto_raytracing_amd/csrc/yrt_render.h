@@ -12,6 +12,35 @@
 
 namespace yrt {
 
+// per-phase GPU time of the last render call: HIP events recorded on the launch
+// stream around every kernel launch of a phase (enabled by yrt_render_params.timing)
+enum render_phase {
+    phase_primary = 0,   // camera rays + closest hit + surface (k_primary)
+    phase_shadow = 1,    // shadow rays, any hit (k_shadow)
+    phase_shade = 2,     // lighting + mirror-ray compaction (k_shade)
+    phase_bounce = 3,    // closest hit of mirror rays (k_bounce)
+    phase_fold = 4,      // reflection fold (k_fold_children)
+    phase_accumulate = 5,
+    phase_megakernel = 6,
+    phase_count = 8
+};
+
+struct phase_timer {
+    bool on = false;
+    std::vector<hipEvent_t> pool;  // start/stop pairs
+    std::vector<int> phase_of;     // per pair
+    size_t used = 0;
+    int begin(int phase, hipStream_t s);  // -1 when off
+    void end(int idx, hipStream_t s);
+    void reset(bool enable) {
+        on = enable;
+        used = 0;
+    }
+    // sums elapsed ms per phase (synchronises the recorded events)
+    void collect(float* ms, int* launches);
+    void destroy();
+};
+
 // one scene resident in one GPU's HBM (a single hipMalloc arena)
 struct device_scene {
     int device = 0;
@@ -22,6 +51,14 @@ struct device_scene {
     int top_depth = 0;    // instance-BVH depth (stack entries needed)
     int shape_depth = 0;  // deepest shape BVH
     size_t ntnodes = 0, nsnodes = 0, nsprims = 0, ninst = 0;
+    size_t max_shape_nodes = 0;
+    bool narrow_stack = true;  // all node indices fit 16-bit stack entries
+    bool reflective = false;   // any material with kr > 0 (bounce levels needed)
+    int nlights = 0;
+    // wavefront workspace (device), grown on demand
+    void* work = nullptr;
+    size_t work_bytes = 0;
+    phase_timer timer;
 };
 
 // Flatten a host scene (with BVH built) into the HBM layout and upload it.
@@ -33,15 +70,18 @@ void device_scene_destroy(device_scene* ds);
 dev_camera make_dev_camera(const camera& c);
 
 // kernels (render.hip)
-hipError_t launch_render(const device_scene& ds, const dev_render_args& args, void* out_rgba,
+hipError_t launch_render(device_scene& ds, const dev_render_args& args, void* out_rgba,
                          unsigned long long* counters, bool count_work, hipStream_t stream);
 hipError_t launch_trace(const device_scene& ds, const float* rays, int n, int any,
                         unsigned char* hit, int* inst, int* ei, float* ew, float* dist,
                         unsigned long long* counters, hipStream_t stream);
 hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, hipStream_t stream);
 
-// stack capacities compiled into the kernels (entries per lane, LDS resident)
-constexpr int top_stack_cap = 24;
-constexpr int shape_stack_cap = 24;
+// traversal stack entries per lane (LDS resident): instance level + shape level
+constexpr int traversal_stack_cap = 40;
+
+// wavefront pipeline (wavefront.hip): same contract as launch_render
+hipError_t launch_render_wavefront(device_scene& ds, const dev_render_args& args, void* out_rgba,
+                                   unsigned long long* counters, bool count_work, bool packet, hipStream_t stream);
 
 }  // namespace yrt
