@@ -1,0 +1,45 @@
+"""Build variants of libyrt.so that differ only in compile-time defines of the
+kernels, for in-process A/B timing (tools/ab_variants.py).
+
+    python tools/build_variants.py scalar:-DYRT_SCALAR_LOADS=1 vec:-DYRT_SCALAR_LOADS=0
+
+writes yocto_raytracing_amd/variants/libyrt_<name>.so (git-ignored, travels to the GPU box).
+"""
+from __future__ import annotations
+
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "yocto_raytracing_amd"
+sys.path.insert(0, str(PKG))
+import build as b  # noqa: E402
+
+
+def main(argv):
+    b.build_library()
+    out_dir = PKG / "variants"
+    out_dir.mkdir(exist_ok=True)
+    host_objs = [b.BUILD / (Path(s).stem + ".o") for s in b.SOURCES if not s.endswith(".hip")]
+    for spec in argv:
+        name, _, defs = spec.partition(":")
+        defines = [d for d in defs.split(",") if d]
+        vdir = out_dir / name
+        vdir.mkdir(exist_ok=True)
+        objs = []
+        for src in b.SOURCES:
+            if not src.endswith(".hip"):
+                continue
+            o = vdir / (Path(src).stem + ".o")
+            subprocess.run([b.HIPCC, *b.COMMON, *defines, f"--offload-arch={b.ARCH}", "-c", str(b.CSRC / src),
+                            "-o", str(o)], check=True, capture_output=True)
+            objs.append(o)
+        lib = out_dir / f"libyrt_{name}.so"
+        subprocess.run([b.HIPCC, "-shared", "-fPIC", f"--offload-arch={b.ARCH}", "-o", str(lib),
+                        *map(str, host_objs + objs), "-lz"], check=True)
+        print(lib)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -477,7 +477,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     const int cap = pix_per_chunk * spp;
     const size_t need = workspace_bytes(cap, ds.nlights, nlevels);
     if (need > ds.work_bytes) {
-        if (ds.work) hipFree(ds.work);
+        if (ds.work) (void)hipFree(ds.work);
         ds.work = nullptr;
         ds.work_bytes = 0;
         hipError_t e = hipMalloc(&ds.work, need);
