@@ -143,30 +143,23 @@ def main():
     yrt.build_bvh(scn)
     ds = scn.upload(local)
 
-    params = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=(BAND, world, rank),
-                               algorithm=a.algorithm)
+    from yocto_raytracing_amd.shard import BandLayout, gather_frame, render_params_band
+
+    params = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, algorithm=a.algorithm)
     W, H = ds.image_size(params)
-    nbands = (H + BAND - 1) // BAND
-    bands_per_rank = (nbands + world - 1) // world
-    local_rows = bands_per_rank * BAND
+    layout = BandLayout(H, world, BAND)
+    band, local_rows = render_params_band(layout, rank)
+    params.band, params.band_stride, params.band_offset = band
     params.tile_h = local_rows  # every rank renders the same padded count (rows past H read 0)
     shard = torch.empty((local_rows, W, 4), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else shard
-    # gathered row r*local_rows + b*BAND + k  <-  image row (b*world + r)*BAND + k
-    src_index = []
-    for r in range(world):
-        for b in range(bands_per_rank):
-            for k in range(BAND):
-                if (b * world + r) * BAND + k < H:
-                    src_index.append(((b * world + r) * BAND + k, r * local_rows + b * BAND + k))
-    src_index.sort()
-    perm = torch.tensor([s for _, s in src_index], device=dev, dtype=torch.long)
+    gathered = torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    index = torch.as_tensor(layout.gather_index(), device=dev)
     frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     # untimed instrumented pass: algorithmic work counts for the roofline bytes
-    pc = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=(BAND, world, rank),
-                           count_work=True, algorithm=a.algorithm)
+    pc = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=band, count_work=True,
+                           algorithm=a.algorithm)
     pc.tile_h = local_rows
     ds.render_into(pc, shard.data_ptr(), stream=stream.cuda_stream)
     work = ds.last_stats()
@@ -183,15 +176,16 @@ def main():
                       work["prim_tests"] * BYTES_PRIM + work["shaded_hits"] * BYTES_HIT +
                       work["texture_lookups"] * BYTES_TEX + local_rows * W * BYTES_PIXEL,
     }
-    kernel_names = {"shadow": "k_shadow<false,u16>", "primary": "k_primary<false,u16>",
-                    "megakernel": "render_kernel<false>"}
+    # rocprof names of the timed (COUNT=false) kernels: <COUNT, PACKET, stack entry>
+    targs = {"wavefront": "<false, true, unsigned int>", "wavefront_lane": "<false, false, unsigned short>"}
+    kernel_names = {"megakernel": "render_kernel<false>"}
+    for ph in ("primary", "shadow", "bounce"):
+        kernel_names[ph] = f"k_{ph}{targs.get(a.algorithm, '')}"
 
     def step(timing=0):
         params.timing = timing
         ds.render_into(params, shard.data_ptr(), stream=stream.cuda_stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, shard)
-        torch.index_select(gathered, 0, perm, out=frame)
+        gather_frame(shard, layout, index, gathered, frame)
 
     for _ in range(a.warmup):
         step()
@@ -230,7 +224,7 @@ def main():
         if tj.exists():
             try:
                 tr = json.loads(tj.read_text())
-                key = f"{a.scene}-r{a.resolution}-s{a.samples}-n{world}-{dom}"
+                key = f"{a.scene}-r{a.resolution}-s{a.samples}-n{world}-{a.algorithm}-{dom}"
                 traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None

@@ -130,3 +130,24 @@ def close_mask(a: np.ndarray, b: np.ndarray, atol=ATOL, rtol=RTOL) -> np.ndarray
 
 def have_reference() -> bool:
     return (REFERENCE / "src" / "raytrace.cpp").exists() and (ROOT / "oracle/_ref/libyrtref.so").exists()
+
+
+def read_png_rgba8(path) -> np.ndarray:
+    """Decode an RGBA8 PNG written by yrt_save_image (filter type 0 on every row)."""
+    import struct
+    import zlib
+
+    data = Path(path).read_bytes()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n = struct.unpack(">I", data[pos:pos + 4])[0]
+        typ = data[pos + 4:pos + 8]
+        if typ == b"IHDR":
+            w, h = struct.unpack(">II", data[pos + 8:pos + 16])
+        elif typ == b"IDAT":
+            idat += data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, w * 4 + 1)
+    assert (raw[:, 0] == 0).all(), "unexpected PNG row filter"
+    return raw[:, 1:].reshape(h, w, 4)

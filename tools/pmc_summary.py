@@ -1,6 +1,6 @@
 """Summarise rocprofv3 counter CSVs into per-kernel HBM traffic per launch.
 
-    python tools/pmc_summary.py --key instance10000-r1080-s8-n1 \
+    python tools/pmc_summary.py --key instance10000-r1080-s8-n1-wavefront \
         --fetch gpurun_out/p3/p3_counter_collection.csv \
         --write gpurun_out/p4/p4_counter_collection.csv \
         [--kernel-trace gpurun_out/ks/ks_kernel_stats.csv] > profiles/pmc_traffic.json
@@ -8,7 +8,7 @@
 HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads (16 B/lane), and
 WRITE_SIZE is exact for 16-B stores (MI355X_MICROARCH.md, HBM section); both come
-from separate --pmc passes. Only the un-instrumented (COUNT=false) kernels are kept.
+from separate --pmc passes. Only the un-instrumented (COUNT=false, first template argument) kernels are kept.
 """
 from __future__ import annotations
 
@@ -35,7 +35,7 @@ def per_launch(path: str, counter: str) -> dict:
         if r["Counter_Name"] != counter:
             continue
         k = short(r["Kernel_Name"])
-        if "true" in k:
+        if re.match(r"\w+<true", k):  # COUNT=true: the instrumented twin
             continue
         vals[k] += float(r["Counter_Value"])
         launches[k].add(r["Dispatch_Id"])

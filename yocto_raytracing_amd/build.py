@@ -36,7 +36,7 @@ HOST_DEFS = ["-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
 
 
 def _headers():
-    return list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    return list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h*"))
 
 
 def _stale(out: Path, deps) -> bool:

@@ -242,9 +242,9 @@ size_t yrt_scene_device_bytes(const yrt_scene* s) { return s && s->ds ? s->ds->a
 
 void yrt_scene_free(yrt_scene* s) {
     if (!s) return;
-    if (s->ds) hipSetDevice(s->ds->device);
-    if (s->counters) hipFree(s->counters);
-    if (s->scratch) hipFree(s->scratch);
+    if (s->ds) (void)hipSetDevice(s->ds->device);
+    if (s->counters) (void)hipFree(s->counters);
+    if (s->scratch) (void)hipFree(s->scratch);
     yrt::device_scene_destroy(s->ds);
     delete s;
 }

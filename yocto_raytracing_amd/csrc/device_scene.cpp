@@ -294,7 +294,7 @@ int phase_timer::begin(int phase, hipStream_t s) {
         hipEvent_t a, b;
         if (hipEventCreate(&a) != hipSuccess) return -1;
         if (hipEventCreate(&b) != hipSuccess) {
-            hipEventDestroy(a);
+            (void)hipEventDestroy(a);
             return -1;
         }
         pool.push_back(a);
@@ -303,12 +303,12 @@ int phase_timer::begin(int phase, hipStream_t s) {
     }
     int idx = (int)used++;
     phase_of[idx] = phase;
-    hipEventRecord(pool[2 * idx], s);
+    (void)hipEventRecord(pool[2 * idx], s);
     return idx;
 }
 
 void phase_timer::end(int idx, hipStream_t s) {
-    if (idx >= 0) hipEventRecord(pool[2 * idx + 1], s);
+    if (idx >= 0) (void)hipEventRecord(pool[2 * idx + 1], s);
 }
 
 void phase_timer::collect(float* ms, int* launches) {
@@ -318,14 +318,14 @@ void phase_timer::collect(float* ms, int* launches) {
     }
     for (size_t i = 0; i < used; i++) {
         float t = 0;
-        hipEventSynchronize(pool[2 * i + 1]);
+        (void)hipEventSynchronize(pool[2 * i + 1]);
         if (hipEventElapsedTime(&t, pool[2 * i], pool[2 * i + 1]) == hipSuccess) ms[phase_of[i]] += t;
         launches[phase_of[i]]++;
     }
 }
 
 void phase_timer::destroy() {
-    for (auto e : pool) hipEventDestroy(e);
+    for (auto e : pool) (void)hipEventDestroy(e);
     pool.clear();
     phase_of.clear();
     used = 0;
@@ -333,10 +333,10 @@ void phase_timer::destroy() {
 
 void device_scene_destroy(device_scene* ds) {
     if (!ds) return;
-    hipSetDevice(ds->device);
+    (void)hipSetDevice(ds->device);
     ds->timer.destroy();
-    if (ds->arena) hipFree(ds->arena);
-    if (ds->work) hipFree(ds->work);
+    if (ds->arena) (void)hipFree(ds->arena);
+    if (ds->work) (void)hipFree(ds->work);
     delete ds;
 }
 
