@@ -124,6 +124,40 @@ int yrt_host_scene_info(const yrt_host_scene* hs, long long* info12);
 int yrt_host_image_size(const yrt_host_scene* hs, int camera, int resolution, int* w, int* h);
 void yrt_host_scene_free(yrt_host_scene* hs);
 
+/* ---- host scene from memory: the reference's scene* built field by field ----
+ * For a host program that already holds a scene (scene.h:26-155) -- e.g. the
+ * reference's own main() after load_scene -- instead of a file. Arrays are copied.
+ * Frames are 12 floats {x.xyz, y.xyz, z.xyz, o.xyz} (frame3f, vmath.h). Indices
+ * returned through `index` are what materials/instances refer to (-1 = none). */
+typedef struct yrt_material_desc { /* material, scene.h:62-86 */
+    float ke[3], kd[3], ks[3], kr[3];
+    float rs;
+    int kd_txt, ks_txt; /* texture index or -1 */
+} yrt_material_desc;
+typedef struct yrt_shape_desc { /* shape, scene.h:26-50; one primitive kind per shape */
+    int npos;
+    const float* pos;      /* npos x 3 */
+    const float* norm;     /* npos x 3 or NULL */
+    const float* texcoord; /* npos x 2 or NULL */
+    const float* radius;   /* npos or NULL (required for points/lines) */
+    int npoints;
+    const int* points;     /* npoints */
+    int nlines;
+    const int* lines;      /* nlines x 2 */
+    int ntriangles;
+    const int* triangles;  /* ntriangles x 3 */
+} yrt_shape_desc;
+int yrt_host_scene_create(yrt_host_scene** out);
+/* camera, scene.h:115-123 */
+int yrt_host_scene_add_camera(yrt_host_scene* hs, const float frame[12], float fovy, float aspect, float aperture,
+                              float focus, int* index);
+/* texture, scene.h:54-58: 8-bit RGBA rows, pixels[j*w+i] */
+int yrt_host_scene_add_texture(yrt_host_scene* hs, int w, int h, const unsigned char* rgba8, int* index);
+int yrt_host_scene_add_material(yrt_host_scene* hs, const yrt_material_desc* m, int* index);
+int yrt_host_scene_add_shape(yrt_host_scene* hs, const yrt_shape_desc* s, int* index);
+/* instance, scene.h:99-111 */
+int yrt_host_scene_add_instance(yrt_host_scene* hs, const float frame[12], int shape, int material, int* index);
+
 /* ---- device scene ---- */
 /* flatten to the HBM layout and upload to `device` (needs a built BVH) */
 int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out);

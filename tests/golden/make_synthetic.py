@@ -1,0 +1,167 @@
+"""Synthetic scene for the primitive kinds the reference's inputs never exercise
+(`in/lines_pointlight` is missing from the reference; no `in/*` scene is hit on a
+point), pinned by the REFERENCE ITSELF:
+
+    make -C oracle ref && python tests/golden/make_synthetic.py
+
+1. builds `scenes/lines.yrtscene` in memory with the product's scene builder
+   (yrt_host_scene_add_*): a triangle floor, hair-like line strips with tapering
+   radius and tangent normals, a cloud of point spheres, a rotated + translated
+   instance of the strands, a textured quad, and two point lights;
+2. has the reference read that file into its own structs (oracle/_ref
+   ref_read_scene -> scene.h types + build_bvh, scene.cpp:554) and render / trace it
+   (raytrace.cpp:213, scene.cpp:483-494), writing `ref_render_lines.npz`,
+   `ref_rays_lines.npz` and the scene/BVH digests into `ref_digests.json`.
+
+Data only; no reference source is copied.
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(HERE))
+
+RENDERS = [(64, 1), (48, 2), (40, 3)]
+
+
+def rot_y(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, -s], [0, 1, 0], [s, 0, c]], np.float32)
+
+
+def frame(rot=None, o=(0, 0, 0)):
+    r = np.eye(3, dtype=np.float32) if rot is None else rot
+    return np.concatenate([r.reshape(-1), np.asarray(o, np.float32)]).astype(np.float32)
+
+
+def build_scene(path: Path):
+    import yocto_raytracing_amd as yrt
+
+    rng = np.random.default_rng(1710)
+    s = yrt.Scene.create()
+    # camera looking at the origin from (0, 3, 8): frame z points back toward the eye
+    eye, target = np.array([0, 3, 8], np.float32), np.zeros(3, np.float32)
+    z = (eye - target) / np.linalg.norm(eye - target)
+    x = np.cross([0, 1, 0], z).astype(np.float32)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x).astype(np.float32)
+    s.add_camera(np.concatenate([x, y, z, eye]), fovy=0.6, aspect=16 / 9, focus=float(np.linalg.norm(eye)))
+
+    tex = np.zeros((64, 64, 4), np.uint8)
+    tex[..., 0] = (np.arange(64)[None, :] * 4).astype(np.uint8)
+    tex[..., 1] = (np.arange(64)[:, None] * 4).astype(np.uint8)
+    tex[(np.arange(64)[:, None] // 8 + np.arange(64)[None, :] // 8) % 2 == 0, 2] = 255
+    tex[..., 3] = 255
+    t0 = s.add_texture(tex)
+
+    m_floor = s.add_material(kd=(0.5, 0.5, 0.45), ks=(0.04, 0.04, 0.04), rs=0.3)
+    m_hair = s.add_material(kd=(0.35, 0.2, 0.1), ks=(0.3, 0.3, 0.3), rs=0.15)
+    m_dots = s.add_material(kd=(0.1, 0.3, 0.6), ks=(0.2, 0.2, 0.2), rs=0.4)
+    m_tex = s.add_material(kd=(0.9, 0.9, 0.9), ks=(0.1, 0.1, 0.1), rs=0.5, kd_txt=t0, ks_txt=t0)
+    m_light = s.add_material(ke=(30, 30, 30))
+    m_light2 = s.add_material(ke=(12, 16, 20))
+
+    # floor: 8x8 grid of quads (2 triangles each) at y = 0
+    g = np.linspace(-6, 6, 9, dtype=np.float32)
+    gx, gz = np.meshgrid(g, g)
+    pos = np.stack([gx.ravel(), np.zeros(81, np.float32), gz.ravel()], 1)
+    tris = []
+    for j in range(8):
+        for i in range(8):
+            a, b, c, d = j * 9 + i, j * 9 + i + 1, (j + 1) * 9 + i + 1, (j + 1) * 9 + i
+            tris += [(a, d, c), (a, c, b)]
+    floor = s.add_shape(pos, norm=np.tile([0, 1, 0], (81, 1)), texcoord=pos[:, [0, 2]] / 12 + 0.5,
+                        triangles=np.array(tris))
+
+    # strands: 60 curly line strips of 10 segments, radius tapering 0.03 -> 0.006
+    P, N, R, UV, L = [], [], [], [], []
+    for k in range(60):
+        base = rng.uniform([-1.5, 0, -1.5], [1.5, 0, 1.5]).astype(np.float32)
+        phase, amp = rng.uniform(0, 6.28), rng.uniform(0.05, 0.25)
+        t = np.linspace(0, 1, 11, dtype=np.float32)
+        p = np.stack([base[0] + amp * np.sin(6 * t + phase), 2.2 * t, base[2] + amp * np.cos(5 * t + phase)], 1)
+        tan = np.gradient(p, axis=0)
+        tan /= np.linalg.norm(tan, axis=1, keepdims=True)
+        off = len(P) and sum(len(q) for q in P)
+        P.append(p)
+        N.append(tan)
+        R.append((0.03 * (1 - t) + 0.006 * t).astype(np.float32))
+        UV.append(np.stack([t, np.full_like(t, k / 60)], 1))
+        L += [(off + i, off + i + 1) for i in range(10)]
+    strands = s.add_shape(np.concatenate(P), norm=np.concatenate(N), texcoord=np.concatenate(UV),
+                          radius=np.concatenate(R), lines=np.array(L))
+
+    # point spheres: 400 dots of radius 0.04-0.08 in a slab above the floor
+    dp = rng.uniform([-4, 0.1, -3], [4, 1.2, 1.5], size=(400, 3)).astype(np.float32)
+    dn = rng.normal(size=(400, 3)).astype(np.float32)
+    dots = s.add_shape(dp, norm=dn, texcoord=rng.uniform(0, 1, (400, 2)), radius=rng.uniform(0.04, 0.08, 400),
+                       points=np.arange(400))
+
+    # a textured upright quad behind the strands
+    qp = np.array([[-2.5, 0, -2.5], [2.5, 0, -2.5], [2.5, 3, -2.5], [-2.5, 3, -2.5]], np.float32)
+    quad = s.add_shape(qp, norm=np.tile([0, 0, 1], (4, 1)), texcoord=[[0, 0], [3, 0], [3, 2], [0, 2]],
+                       triangles=[[0, 1, 2], [0, 2, 3]])
+
+    # point lights: single points of radius 0.001 (the reference's `p` light shapes)
+    light = s.add_shape([[0, 0, 0]], norm=[[0, 0, 1]], texcoord=[[0, 0]], radius=[0.001], points=[0])
+
+    s.add_instance(frame(), floor, m_floor)
+    s.add_instance(frame(), strands, m_hair)
+    s.add_instance(frame(rot_y(0.7), (2.6, 0, 0.4)), strands, m_hair)
+    s.add_instance(frame(), dots, m_dots)
+    s.add_instance(frame(), quad, m_tex)
+    s.add_instance(frame(o=(2, 6, 4)), light, m_light)
+    s.add_instance(frame(o=(-4, 5, 1)), light, m_light2)
+    s.save(str(path))
+    return s
+
+
+def main():
+    from make_golden import load_ref, sample_rays, trace
+
+    spath = HERE / "scenes" / "lines.yrtscene"
+    build_scene(spath)
+    lib = load_ref()
+    lib.ref_read_scene.restype = lib.ref_load_scene.restype
+    lib.ref_read_scene.argtypes = lib.ref_load_scene.argtypes
+    scn = lib.ref_read_scene(str(spath).encode())
+    assert scn, "reference could not read the synthetic scene"
+    bpath = Path("/tmp/lines_ref.yrtbvh")
+    lib.ref_write_bvh(scn, str(bpath).encode())
+    # the reference re-serialises what it read: the file must round-trip unchanged
+    rpath = Path("/tmp/lines_ref.yrtscene")
+    lib.ref_write_scene(scn, str(rpath).encode())
+    assert gzip.open(rpath).read() == gzip.open(spath).read(), "reference read-back differs"
+    dig = json.loads((HERE / "ref_digests.json").read_text())
+    dig["lines"] = {"scene_sha256": hashlib.sha256(gzip.open(spath).read()).hexdigest(),
+                    "bvh_sha256": hashlib.sha256(gzip.open(bpath).read()).hexdigest()}
+    (HERE / "ref_digests.json").write_text(json.dumps(dig, indent=1) + "\n")
+    import ctypes as C
+
+    out = {}
+    for res, sp in RENDERS:
+        w, h = C.c_int(), C.c_int()
+        lib.ref_image_size(scn, res, C.byref(w), C.byref(h))
+        img = np.zeros((h.value, w.value, 4), np.float32)
+        out[f"rays_r{res}_s{sp}"] = np.int64(lib.ref_render(scn, 0.1, res, sp, img.ctypes.data))
+        out[f"img_r{res}_s{sp}"] = img
+    np.savez_compressed(HERE / "ref_render_lines.npz", **out)
+    rays = sample_rays(lib, scn, np.random.default_rng(99))
+    hit, inst, ei, ew, dist = trace(lib, scn, rays, False)
+    ahit = trace(lib, scn, rays, True)[0]
+    np.savez_compressed(HERE / "ref_rays_lines.npz", rays=rays, hit=hit, inst=inst, ei=ei, ew=ew, dist=dist,
+                        any_hit=ahit)
+    print("lines", dig["lines"], "hit fraction", hit.mean(), "any", ahit.mean())
+
+
+if __name__ == "__main__":
+    main()

@@ -14,7 +14,10 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent.parent
 GOLDEN = ROOT / "tests" / "golden"
 SCENES = GOLDEN / "scenes"
-SCENE_NAMES = ("basic", "simple", "refl", "instance10000")
+# the reference's four `in/*` scenes + "lines", a synthetic lines/points/texture scene
+# built by tests/golden/make_synthetic.py and rendered by the reference itself
+SCENE_NAMES = ("basic", "simple", "refl", "instance10000", "lines")
+OBJ_SCENES = ("basic", "simple", "refl", "instance10000")
 REFERENCE = Path("/root/reference")
 REF_OBJ = {
     "basic": REFERENCE / "in/basic_pointlight/basic_pointlight.obj",

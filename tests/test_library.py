@@ -9,7 +9,7 @@ import re
 import numpy as np
 import pytest
 
-from helpers import REF_OBJ, ROOT, SCENE_NAMES, digests, have_reference, scene_path
+from helpers import OBJ_SCENES, REF_OBJ, ROOT, SCENE_NAMES, digests, have_reference, scene_path
 
 
 @pytest.fixture(scope="module")
@@ -80,7 +80,7 @@ def test_scene_info(yrt):
 
 @pytest.mark.reference
 @pytest.mark.skipif(not have_reference(), reason="needs /root/reference and oracle/_ref")
-@pytest.mark.parametrize("name", SCENE_NAMES)
+@pytest.mark.parametrize("name", OBJ_SCENES)
 def test_obj_loader_matches_reference_loader(yrt, name, tmp_path):
     s = yrt.load_scene(str(REF_OBJ[name]))
     out = tmp_path / "x.yrtscene"

@@ -53,6 +53,81 @@ class Scene:
         except Exception:
             pass
 
+    # ---- building a scene in memory (yrt_host_scene_add_*: the reference's scene*
+    # filled field by field, scene.h:26-155) ----
+    @classmethod
+    def create(cls) -> "Scene":
+        h = C.c_void_p()
+        check(N.lib.yrt_host_scene_create(C.byref(h)), "yrt_host_scene_create")
+        return cls(h.value)
+
+    @staticmethod
+    def _frame(frame) -> np.ndarray:
+        f = np.ascontiguousarray(frame, np.float32).reshape(-1)
+        if f.size != 12:
+            raise ValueError("frame must be 12 floats: x.xyz, y.xyz, z.xyz, o.xyz")
+        return f
+
+    def _added(self, status, what, idx) -> int:
+        check(status, what)
+        for ds in self._device_scenes.values():
+            ds.close()
+        self._device_scenes.clear()
+        return idx.value
+
+    def add_camera(self, frame, fovy: float, aspect: float, focus: float, aperture: float = 0.0) -> int:
+        f, idx = self._frame(frame), C.c_int()
+        return self._added(N.lib.yrt_host_scene_add_camera(self._h, f.ctypes.data, fovy, aspect, aperture, focus,
+                                                           C.byref(idx)), "add_camera", idx)
+
+    def add_texture(self, rgba8: np.ndarray) -> int:
+        t = np.ascontiguousarray(rgba8, np.uint8)
+        if t.ndim != 3 or t.shape[2] != 4:
+            raise ValueError("texture must be (h, w, 4) uint8")
+        idx = C.c_int()
+        return self._added(N.lib.yrt_host_scene_add_texture(self._h, t.shape[1], t.shape[0], t.ctypes.data,
+                                                            C.byref(idx)), "add_texture", idx)
+
+    def add_material(self, kd=(0, 0, 0), ks=(0, 0, 0), kr=(0, 0, 0), ke=(0, 0, 0), rs: float = 0.0,
+                     kd_txt: int = -1, ks_txt: int = -1) -> int:
+        m = N.MaterialDesc()
+        for name, v in (("ke", ke), ("kd", kd), ("ks", ks), ("kr", kr)):
+            getattr(m, name)[:] = [float(x) for x in v]
+        m.rs, m.kd_txt, m.ks_txt = float(rs), int(kd_txt), int(ks_txt)
+        idx = C.c_int()
+        return self._added(N.lib.yrt_host_scene_add_material(self._h, C.byref(m), C.byref(idx)), "add_material", idx)
+
+    def add_shape(self, pos, norm=None, texcoord=None, radius=None, points=None, lines=None, triangles=None) -> int:
+        keep = []
+
+        def arr(a, dtype, cols):
+            if a is None:
+                return None, 0
+            x = np.ascontiguousarray(a, dtype)
+            x = x.reshape(-1, cols) if cols > 1 else x.reshape(-1)
+            keep.append(x)
+            return x.ctypes.data, x.shape[0]
+
+        d = N.ShapeDesc()
+        d.pos, d.npos = arr(pos, np.float32, 3)
+        d.norm, _ = arr(norm, np.float32, 3)
+        d.texcoord, _ = arr(texcoord, np.float32, 2)
+        d.radius, _ = arr(radius, np.float32, 1)
+        d.points, d.npoints = arr(points, np.int32, 1)
+        d.lines, d.nlines = arr(lines, np.int32, 2)
+        d.triangles, d.ntriangles = arr(triangles, np.int32, 3)
+        for name, n in (("norm", 3), ("texcoord", 2), ("radius", 1)):
+            a = locals()[name]
+            if a is not None and np.asarray(a).size != d.npos * n:
+                raise ValueError(f"{name} must have one entry per vertex")
+        idx = C.c_int()
+        return self._added(N.lib.yrt_host_scene_add_shape(self._h, C.byref(d), C.byref(idx)), "add_shape", idx)
+
+    def add_instance(self, frame, shape: int, material: int) -> int:
+        f, idx = self._frame(frame), C.c_int()
+        return self._added(N.lib.yrt_host_scene_add_instance(self._h, f.ctypes.data, shape, material, C.byref(idx)),
+                           "add_instance", idx)
+
     def info(self) -> dict:
         buf = (C.c_longlong * 12)()
         check(N.lib.yrt_host_scene_info(self._h, buf), "yrt_host_scene_info")

@@ -60,7 +60,19 @@ class Timings(C.Structure):
     _fields_ = [("ms", C.c_float * 8), ("launches", C.c_int * 8)]
 
 
+class MaterialDesc(C.Structure):
+    _fields_ = [("ke", C.c_float * 3), ("kd", C.c_float * 3), ("ks", C.c_float * 3), ("kr", C.c_float * 3),
+                ("rs", C.c_float), ("kd_txt", C.c_int), ("ks_txt", C.c_int)]
+
+
+class ShapeDesc(C.Structure):
+    _fields_ = [("npos", C.c_int), ("pos", C.c_void_p), ("norm", C.c_void_p), ("texcoord", C.c_void_p),
+                ("radius", C.c_void_p), ("npoints", C.c_int), ("points", C.c_void_p), ("nlines", C.c_int),
+                ("lines", C.c_void_p), ("ntriangles", C.c_int), ("triangles", C.c_void_p)]
+
+
 _vp = C.c_void_p
+_ip = C.POINTER(C.c_int)
 _sig = {
     "yrt_abi_version": (C.c_int, []),
     "yrt_status_string": (C.c_char_p, [C.c_int]),
@@ -73,6 +85,12 @@ _sig = {
     "yrt_host_scene_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
     "yrt_host_image_size": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "yrt_host_scene_free": (None, [_vp]),
+    "yrt_host_scene_create": (C.c_int, [C.POINTER(_vp)]),
+    "yrt_host_scene_add_camera": (C.c_int, [_vp, _vp, C.c_float, C.c_float, C.c_float, C.c_float, _ip]),
+    "yrt_host_scene_add_texture": (C.c_int, [_vp, C.c_int, C.c_int, _vp, _ip]),
+    "yrt_host_scene_add_material": (C.c_int, [_vp, C.POINTER(MaterialDesc), _ip]),
+    "yrt_host_scene_add_shape": (C.c_int, [_vp, C.POINTER(ShapeDesc), _ip]),
+    "yrt_host_scene_add_instance": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _ip]),
     "yrt_scene_upload": (C.c_int, [_vp, C.c_int, C.POINTER(_vp)]),
     "yrt_scene_device_bytes": (C.c_size_t, [_vp]),
     "yrt_scene_free": (None, [_vp]),

@@ -104,6 +104,20 @@ resolved_window resolve(const yrt::device_scene& ds, const yrt_render_params& p)
 
 }  // namespace
 
+namespace {
+yrt::frame3f frame_of(const float* f) {
+    return {{f[0], f[1], f[2]}, {f[3], f[4], f[5]}, {f[6], f[7], f[8]}, {f[9], f[10], f[11]}};
+}
+// a scene edited after build_bvh needs a new build before upload
+template <typename T>
+int append(yrt_host_scene* hs, std::vector<T>& v, T&& item, int* index) {
+    v.push_back(std::move(item));
+    hs->scn.has_bvh = false;
+    if (index) *index = (int)v.size() - 1;
+    return YRT_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int yrt_abi_version(void) { return YRT_ABI_VERSION; }
@@ -213,6 +227,116 @@ int yrt_host_image_size(const yrt_host_scene* hs, int camera, int resolution, in
 }
 
 void yrt_host_scene_free(yrt_host_scene* hs) { delete hs; }
+
+int yrt_host_scene_create(yrt_host_scene** out) {
+    if (!out) return YRT_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        *out = new yrt_host_scene();
+        return YRT_OK;
+    });
+}
+
+
+int yrt_host_scene_add_camera(yrt_host_scene* hs, const float frame[12], float fovy, float aspect, float aperture,
+                              float focus, int* index) {
+    if (!hs || !frame) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::camera c;
+        c.frame = frame_of(frame);
+        c.fovy = fovy, c.aspect = aspect, c.aperture = aperture, c.focus = focus;
+        return append(hs, hs->scn.cameras, std::move(c), index);
+    });
+}
+
+int yrt_host_scene_add_texture(yrt_host_scene* hs, int w, int h, const unsigned char* rgba8, int* index) {
+    if (!hs || !rgba8 || w <= 0 || h <= 0) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::texture t;
+        t.width = w, t.height = h;
+        t.pixels.resize((size_t)w * h);
+        memcpy(t.pixels.data(), rgba8, (size_t)w * h * 4);
+        return append(hs, hs->scn.textures, std::move(t), index);
+    });
+}
+
+int yrt_host_scene_add_material(yrt_host_scene* hs, const yrt_material_desc* d, int* index) {
+    if (!hs || !d) return YRT_ERR_INVALID_ARG;
+    const int nt = (int)hs->scn.textures.size();
+    if (d->kd_txt < -1 || d->kd_txt >= nt || d->ks_txt < -1 || d->ks_txt >= nt) {
+        g_last_error = "material texture index out of range";
+        return YRT_ERR_INVALID_ARG;
+    }
+    return guarded([&] {
+        yrt::material m;
+        m.ke = {d->ke[0], d->ke[1], d->ke[2]};
+        m.kd = {d->kd[0], d->kd[1], d->kd[2]};
+        m.ks = {d->ks[0], d->ks[1], d->ks[2]};
+        m.kr = {d->kr[0], d->kr[1], d->kr[2]};
+        m.rs = d->rs;
+        m.kd_txt = d->kd_txt, m.ks_txt = d->ks_txt;
+        return append(hs, hs->scn.materials, std::move(m), index);
+    });
+}
+
+int yrt_host_scene_add_shape(yrt_host_scene* hs, const yrt_shape_desc* d, int* index) {
+    if (!hs || !d || d->npos < 0 || d->npoints < 0 || d->nlines < 0 || d->ntriangles < 0 ||
+        (d->npos && !d->pos) || (d->npoints && !d->points) || (d->nlines && !d->lines) ||
+        (d->ntriangles && !d->triangles))
+        return YRT_ERR_INVALID_ARG;
+    const int kinds = (d->npoints > 0) + (d->nlines > 0) + (d->ntriangles > 0);
+    if (kinds > 1) {
+        g_last_error = "shape mixes primitive types (unsupported)";
+        return YRT_ERR_UNSUPPORTED;
+    }
+    if ((d->npoints || d->nlines) && !d->radius) {
+        g_last_error = "points/lines need a radius per vertex";
+        return YRT_ERR_INVALID_ARG;
+    }
+    auto bad = [&](const int* e, long long n) {
+        for (long long k = 0; k < n; k++)
+            if (e[k] < 0 || e[k] >= d->npos) return true;
+        return false;
+    };
+    if (bad(d->points, d->npoints) || bad(d->lines, 2ll * d->nlines) || bad(d->triangles, 3ll * d->ntriangles)) {
+        g_last_error = "element index outside the vertex array";
+        return YRT_ERR_INVALID_ARG;
+    }
+    return guarded([&] {
+        yrt::shape s;
+        const size_t n = (size_t)d->npos;
+        s.pos.resize(n);
+        memcpy(s.pos.data(), d->pos, n * 12);
+        if (d->norm) {
+            s.norm.resize(n);
+            memcpy(s.norm.data(), d->norm, n * 12);
+        }
+        if (d->texcoord) {
+            s.texcoord.resize(n);
+            memcpy(s.texcoord.data(), d->texcoord, n * 8);
+        }
+        if (d->radius) s.radius.assign(d->radius, d->radius + n);
+        s.points.assign(d->points, d->points + d->npoints);
+        s.lines.resize(d->nlines);
+        if (d->nlines) memcpy(s.lines.data(), d->lines, (size_t)d->nlines * 8);
+        s.triangles.resize(d->ntriangles);
+        if (d->ntriangles) memcpy(s.triangles.data(), d->triangles, (size_t)d->ntriangles * 12);
+        return append(hs, hs->scn.shapes, std::move(s), index);
+    });
+}
+
+int yrt_host_scene_add_instance(yrt_host_scene* hs, const float frame[12], int shape, int material, int* index) {
+    if (!hs || !frame || shape < 0 || shape >= (int)hs->scn.shapes.size() || material < 0 ||
+        material >= (int)hs->scn.materials.size())
+        return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::instance i;
+        i.frame = frame_of(frame);
+        i.shp = shape;
+        i.mat = material;
+        return append(hs, hs->scn.instances, std::move(i), index);
+    });
+}
 
 int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out) {
     if (!hs || !out) return YRT_ERR_INVALID_ARG;
