@@ -8,6 +8,7 @@
 //   yrt_host_scene* yrt_from_reference_scene(const scene*)     scene.h:26-155 -> yrt.h builder
 //   image4f raytrace_gpu(const scene*, const vec3f&, int, int) same signature as raytrace(),
 //                                                               src/raytrace.cpp:213
+//   void raytrace_gpu_release(const scene*)                     drop the scene's device copy
 #include "scene.h"
 #include "yrt.h"
 
@@ -83,10 +84,20 @@ yrt_host_scene* yrt_from_reference_scene(const scene* scn) {
     return hs;
 }
 
+// device copies, one per scene, made on first use and kept until released
+static std::unordered_map<const scene*, yrt_scene*> resident;
+
+// drop the device copy of `scn` (call before deleting or editing the scene)
+void raytrace_gpu_release(const scene* scn) {
+    auto it = resident.find(scn);
+    if (it == resident.end()) return;
+    yrt_scene_free(it->second);
+    resident.erase(it);
+}
+
 // raytrace() (src/raytrace.cpp:213) on the GPU: same arguments, same image4f. The
 // device copy of each scene is made once and reused by later calls.
 image4f raytrace_gpu(const scene* scn, const vec3f& amb, int resolution, int samples) {
-    static std::unordered_map<const scene*, yrt_scene*> resident;
     auto& ds = resident[scn];
     if (!ds) {
         yrt_host_scene* hs = yrt_from_reference_scene(scn);
@@ -129,6 +140,8 @@ int ref_int_save_bvh(void* refscn, const char* path) {
     yrt_host_scene_free(hs);
     return rc;
 }
+
+void ref_int_release(void* refscn) { raytrace_gpu_release((const scene*)refscn); }
 
 int ref_int_render(void* refscn, float amb, int resolution, int samples, float* out) {
     image4f img = raytrace_gpu((const scene*)refscn, {amb, amb, amb}, resolution, samples);

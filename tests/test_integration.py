@@ -28,6 +28,7 @@ def int_lib():
     lib.ref_int_save_bvh.argtypes = [C.c_void_p, C.c_char_p]
     lib.ref_int_render.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_int, C.c_void_p]
     lib.ref_free_scene.argtypes = [C.c_void_p]
+    lib.ref_int_release.argtypes = [C.c_void_p]
     return lib
 
 
@@ -62,6 +63,7 @@ def test_raytrace_gpu_from_reference_scene(name):
         img = np.zeros_like(ref)
         assert lib.ref_int_render(scn, 0.1, res, spp, img.ctypes.data) == 0
     finally:
+        lib.ref_int_release(scn)  # the device copy is keyed by the scene's address
         lib.ref_free_scene(scn)
     assert close_mask(img, ref).all()
     assert np.mean(img.view(np.uint32) == ref.view(np.uint32)) > 0.99
