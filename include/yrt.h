@@ -83,6 +83,9 @@ typedef struct yrt_stats {
     unsigned long long shadow_box_tests;        /* count_work only */
     unsigned long long shadow_instance_entries; /* count_work only */
     unsigned long long shadow_prim_tests;       /* count_work only */
+    unsigned long long wave_node_visits;        /* count_work, packet walk: node steps per wave */
+    unsigned long long wave_prim_visits;        /* count_work, packet walk: primitive steps per wave */
+    unsigned long long shadow_wave_node_visits; /* the same, shadow-ray phase alone */
 } yrt_stats;
 
 /* GPU time per kernel phase of the last render (HIP events on the launch stream) */

@@ -50,7 +50,8 @@ class Stats(C.Structure):
     _fields_ = [(n, C.c_ulonglong) for n in (
         "rays", "camera_samples", "depth_truncated", "stack_overflow", "box_tests",
         "instance_entries", "prim_tests", "shaded_hits", "texture_lookups", "shadow_rays",
-        "shadow_box_tests", "shadow_instance_entries", "shadow_prim_tests")]
+        "shadow_box_tests", "shadow_instance_entries", "shadow_prim_tests", "wave_node_visits",
+        "wave_prim_visits", "shadow_wave_node_visits")]
 
 
 PHASES = ("primary", "shadow", "shade", "bounce", "fold", "accumulate", "megakernel", "unused")

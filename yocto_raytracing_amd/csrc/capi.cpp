@@ -351,8 +351,8 @@ int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out) {
         auto s = new yrt_scene();
         try {
             s->ds = yrt::device_scene_create(hs->scn, device);
-            hip_check(hipMalloc(&s->counters, yrt::cnt_count * sizeof(unsigned long long)), "hipMalloc(counters)");
-            hip_check(hipMemset(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long)), "hipMemset");
+            hip_check(hipMalloc(&s->counters, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long)), "hipMalloc(counters)");
+            hip_check(hipMemset(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long)), "hipMemset");
         } catch (...) {
             yrt_scene_free(s);
             throw;
@@ -418,7 +418,7 @@ int yrt_render(yrt_scene* s, const yrt_render_params* p, float* out, int mem, vo
         if (a.out_stride < r.tw) throw std::invalid_argument("out_stride smaller than the window width");
         size_t bytes = (size_t)a.out_stride * r.th * 4 * sizeof(float);
         void* dst = mem == YRT_MEM_DEVICE ? (void*)out : scratch(s, bytes);
-        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
+        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
         // timing 1: start a new record; 2: keep accumulating across calls (bench loops)
         if (!(p->timing == 2 && s->ds->timer.on)) s->ds->timer.reset(p->timing != 0);
         if (p->algorithm == YRT_ALGO_MEGAKERNEL)
@@ -445,7 +445,7 @@ static int trace_impl(yrt_scene* s, const float* rays, int n, int any, unsigned 
     return guarded([&] {
         hipStream_t st = (hipStream_t)stream;
         hip_check(hipSetDevice(s->ds->device), "hipSetDevice");
-        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
+        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
         s->last_stream = st;
         if (n == 0) return YRT_OK;
         if (mem == YRT_MEM_DEVICE) {
@@ -487,11 +487,17 @@ int yrt_trace_any(yrt_scene* s, const float* rays, int n, unsigned char* hit, in
 int yrt_last_stats(yrt_scene* s, yrt_stats* out) {
     if (!s || !out) return YRT_ERR_INVALID_ARG;
     return guarded([&] {
-        unsigned long long c[yrt::cnt_count];
+        std::vector<unsigned long long> lines((size_t)yrt::cnt_slots * yrt::cnt_count);
         hip_check(hipSetDevice(s->ds->device), "hipSetDevice");
         hip_check(hipStreamSynchronize(s->last_stream), "hipStreamSynchronize");
-        hip_check(hipMemcpy(c, s->counters, sizeof c, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
-        out->rays = c[yrt::cnt_rays];
+        hip_check(hipMemcpy(lines.data(), s->counters, lines.size() * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost),
+                  "hipMemcpy(counters)");
+        unsigned long long c[yrt::cnt_count] = {};
+        for (int l = 0; l < yrt::cnt_slots; l++)
+            for (int k = 0; k < yrt::cnt_count; k++) c[k] += lines[(size_t)l * yrt::cnt_count + k];
+        // the wavefront path counts its shadow rays only under cnt_shadow_rays
+        out->rays = c[yrt::cnt_rays] + c[yrt::cnt_shadow_rays];
         out->camera_samples = c[yrt::cnt_samples];
         out->depth_truncated = c[yrt::cnt_depth_truncated];
         out->stack_overflow = c[yrt::cnt_stack_overflow];
@@ -504,6 +510,9 @@ int yrt_last_stats(yrt_scene* s, yrt_stats* out) {
         out->shadow_box_tests = c[yrt::cnt_shadow_box_tests];
         out->shadow_instance_entries = c[yrt::cnt_shadow_inst_entries];
         out->shadow_prim_tests = c[yrt::cnt_shadow_prim_tests];
+        out->wave_node_visits = c[yrt::cnt_wave_node_visits];
+        out->wave_prim_visits = c[yrt::cnt_wave_prim_visits];
+        out->shadow_wave_node_visits = c[yrt::cnt_shadow_wave_node_visits];
         return YRT_OK;
     });
 }

@@ -185,7 +185,11 @@ device_scene* device_scene_create(const scene& scn, int device) {
         tinst.push_back({f.x.x, f.x.y, f.x.z, as_float(ist.shp)});
         tinst.push_back({f.y.x, f.y.y, f.y.z, as_float(ii)});
         tinst.push_back({f.z.x, f.z.y, f.z.z, as_float(ist.mat)});
-        tinst.push_back({f.o.x, f.o.y, f.o.z, 0});
+        // .w of the last row: the shape's root node and primitive kind, so a traversal
+        // entering the instance needs no dependent fetch of the shape record
+        const i4 sh = shapes[ist.shp];
+        if (sh.x >= (1 << 30)) throw std::runtime_error("scene too large (shape nodes >= 2^30, unsupported)");
+        tinst.push_back({f.o.x, f.o.y, f.o.z, as_float((int)((uint32_t)sh.x | ((uint32_t)sh.y << 30)))});
     }
 
     // ---- materials, lights, textures ----

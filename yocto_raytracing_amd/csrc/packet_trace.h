@@ -12,160 +12,252 @@
 // (src/scene.cpp:386-479) -- closest-hit tie-breaking included. Lanes only idle on
 // nodes that other lanes of the wave need.
 //
-// Why on CDNA4: the node index, the node record, the instance frame and the
-// primitive record of a step are wave-uniform, so they are scalar loads into SGPRs
-// (one request per wave, no per-lane stack, no address VGPRs); the loop control is
-// uniform, so there is no exec-mask divergence at all; per-lane state is just the
-// ray, the local ray and the hit record. Rays of one wave are 64 samples of one
-// pixel (or an 8x8 pixel tile), so the union of their paths is barely larger than
-// one path.
+// One tmax per lane: the reference copies the world tmax into the local ray on
+// instance entry and writes the shape's hit distance back when the shape returns
+// (scene.cpp:468-471); nothing reads the world value in between, so keeping a
+// single value is the same computation. A lane whose tmax became NaN (a NaN hit
+// distance passes both range checks, and only a later hit in the SAME leaf can
+// replace it) fails every later slab test in the reference: it leaves the walk when
+// the leaf is done.
 //
-// Contract: must be called by every lane of the wave in uniform control flow;
-// lanes with valid == false take no part (they get no hit).
+// Shaped for CDNA4's issue model (one scalar unit per CU, 64-wide VALU):
+//  * everything that steers the walk is wave-uniform and lives in SGPRs: node
+//    index, lane masks, stack pointer, instance range, shape root/kind;
+//  * the stack lives in three VGPRs used as 64 lane-indexed slots (slot s = lane s):
+//    a push is a compare + three selects, a pop three v_readlane with the stack
+//    pointer as the lane index -- no LDS round trip, no exec-masked store;
+//  * every branch is on an SGPR value (no exec-mask divergence in the walk) and the
+//    primitive tests are branchless (the reference's early returns become one
+//    predicate);
+//  * an instance record carries its shape's root node and primitive kind, so
+//    entering an instance costs the four frame fetches and no dependent fetch.
+// Rays of a wave are 64 samples of one pixel (or an 8x8 pixel tile), so the union
+// of their paths is barely larger than one path.
+//
+// Contract: called by every lane of the wave in uniform control flow; lanes with
+// valid == false take no part (they report no hit). Stack depth <= 64 (the host
+// rejects scenes whose instance + shape BVH depth exceeds traversal_stack_cap).
 #pragma once
 
 #include "trace_common.h"
 
 namespace yrt {
 
-// per-wave stack in LDS: entry s = {node, lane mask}
-struct wave_stack {
-    int* node;
-    unsigned long long* mask;
-};
-
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ unsigned long long uniform64(unsigned long long x) {
-    unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x);
-    unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
-    return (unsigned long long)hi << 32 | lo;
-}
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float4 lane_value(float4 v, int l) {
+    return {lane_value(v.x, l), lane_value(v.y, l), lane_value(v.z, l), lane_value(v.w, l)};
+}
+
+#ifndef YRT_FEW_LANE_LOADS
+#define YRT_FEW_LANE_LOADS 0
+#endif
+// N consecutive 16-byte records at a wave-uniform address, for every lane. A load
+// that all 64 lanes issue for the same address still costs the vector-memory pipe
+// a full wave's address processing and a 1 KiB data return; here lanes 0..N-1 fetch
+// one record each (one instruction, N active lanes) and v_readlane broadcasts them
+// into SGPRs, which the VALU reads directly as scalar operands.
+template <int N>
+__device__ __forceinline__ void ld_uniform(const f4* p, float4 (&out)[N]) {
+#if YRT_FEW_LANE_LOADS
+    const int lane = __lane_id();
+    float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (lane < N) v = *reinterpret_cast<const float4*>(p + lane);
+#pragma unroll
+    for (int k = 0; k < N; k++) out[k] = lane_value(v, k);
+#else
+    // all N records in flight before anything consumes them; the empty asm pins all
+    // their lanes (no narrowed loads, no .w reload sunk into a later branch)
+#pragma unroll
+    for (int k = 0; k < N; k++) out[k] = *reinterpret_cast<const float4*>(p + k);
+    if constexpr (N == 2)
+        asm volatile("" : "+v"(out[0].x), "+v"(out[0].y), "+v"(out[0].z), "+v"(out[0].w), "+v"(out[1].x),
+                     "+v"(out[1].y), "+v"(out[1].z), "+v"(out[1].w));
+    if constexpr (N == 3)
+        asm volatile("" : "+v"(out[0].x), "+v"(out[0].y), "+v"(out[0].z), "+v"(out[0].w), "+v"(out[1].x),
+                     "+v"(out[1].y), "+v"(out[1].z), "+v"(out[1].w), "+v"(out[2].x), "+v"(out[2].y),
+                     "+v"(out[2].z), "+v"(out[2].w));
+    if constexpr (N == 4)
+        asm volatile("" : "+v"(out[0].x), "+v"(out[0].y), "+v"(out[0].z), "+v"(out[0].w), "+v"(out[1].x),
+                     "+v"(out[1].y), "+v"(out[1].z), "+v"(out[1].w), "+v"(out[2].x), "+v"(out[2].y),
+                     "+v"(out[2].z), "+v"(out[2].w), "+v"(out[3].x), "+v"(out[3].y), "+v"(out[3].z),
+                     "+v"(out[3].w));
+#endif
+}
+
+// intersect_triangle (scene.cpp:229-263) without branches: the same values in the
+// same order; the early returns become one predicate (a NaN w1/w2/t passes its
+// range checks exactly as it does in the reference)
+__device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float tmax, vec3f v0, vec3f e1, vec3f e2,
+                                           float& t, float& w1, float& w2) {
+    vec3f r = cross(d, e2);
+    float den = dot(r, e1);
+    float inv_den = 1.0f / den;
+    vec3f c = o - v0;
+    w1 = dot(r, c) * inv_den;
+    vec3f s = cross(c, e1);
+    w2 = dot(s, d) * inv_den;
+    t = dot(s, e2) * inv_den;
+    return (den != 0) & !(w1 < 0 || w1 > 1) & !(w2 < 0.0f || w1 + w2 > 1.0f) & !(t < tmin || t > tmax);
+}
 
 template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool packet_trace(const dev_scene_view& S, ray3 wray, bool valid, hit_record& hr,
-                                             wave_stack st, work_counts& wc) {
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
+                                             work_counts& wc) {
+    const int lane = __lane_id();
     const unsigned long long me = 1ull << lane;
     // a NaN tmin/tmax fails every slab test of the reference: such a ray never enters a node
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
-    bool hit = false;
     if (!live) return false;
-    const vec3f winvd = {1.0f / wray.d.x, 1.0f / wray.d.y, 1.0f / wray.d.z};
-    vec3f lo_o = wray.o, ld = wray.d, linvd = winvd;  // local ray of the current instance
-    float ltmax = wray.tmax;
-    unsigned long long done = 0;       // any-hit: lanes that already found their hit
+    const vec3f wo = wray.o, wd = wray.d;
+    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    const float tmin = wray.tmin;
+    float tmax = wray.tmax;
+    vec3f co = wo, cd = wd, ci = wi;  // ray of the current level (local inside an instance)
+    // per-lane flags are kept as ints (VGPRs): a bool carried around the loop becomes
+    // a 64-bit lane mask merged with exec on every back edge (scalar work per step)
+    int hit = 0;
+    // the stack: slot s of each of these VGPRs is lane s
+    int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
+    unsigned long long done = 0;       // lanes out of the walk (any-hit found / NaN tmax)
     unsigned long long inst_mask = 0;  // lanes entering the current instance leaf
     int level = 0, sp = 0, base = 0, root = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
     int node = 0;
+    const f4* nbase = S.tnodes;  // node array of the current level (the shape's nodes at level 1)
     unsigned long long mask = live;
     for (;;) {
         // ---- every lane of `mask` tests `node` with its own ray ----
-        const f4* nb = level ? S.snodes + 2 * (root + node) : S.tnodes + 2 * node;
-        const float4 lo = ld4(nb), hi = ld4(nb + 1);
-        bool pass;
-        if (level)
-            pass = !is_nan(ltmax) && box_hit(lo_o, linvd, wray.tmin, ltmax, lo, hi);
-        else
-            pass = !is_nan(wray.tmax) && box_hit(wray.o, winvd, wray.tmin, wray.tmax, lo, hi);
+        const f4* nb = nbase + 2 * node;
+        float4 rec[2];
+        ld_uniform<2>(nb, rec);
+        const float4 lo = rec[0], hi = rec[1];
         if (COUNT && (mask & me)) wc.box++;
-        const unsigned long long pm = ballot(pass) & mask;
-        bool descend = false;
+        if (COUNT && lane == 0) wc.wnode++;
+        const unsigned long long pm = ballot(box_hit(co, ci, tmin, tmax, lo, hi)) & mask;
+#ifdef YRT_EXP_VALU2  // diagnostic: a second, unused box test per step
+        {
+            bool b2 = box_hit(co, ci, tmin * 0.5f, tmax * 0.5f, lo, hi);
+            asm volatile("" ::"v"((int)b2));
+        }
+#endif
+#ifdef YRT_EXP_SALU  // diagnostic: 16 dependent scalar adds per step
+        {
+            int d = node;
+            asm volatile(
+                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
+                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
+                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
+                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
+                : "+s"(d));
+        }
+#endif
+#ifdef YRT_EXP_LAT  // diagnostic: one more dependent fetch per step
+        {
+            float4 again = ld4_whole(nbase + 2 * (node ^ (int)(pm & 1)));
+            asm volatile("" ::"v"(again.x));
+        }
+#endif
         if (pm) {
             const int start = uniform(ibits(lo.w));
             const uint32_t cl = (uint32_t)uniform((int)ubits(hi.w));
-            const int count = (int)(cl & 0xffffu);
             if (!(cl & leaf_bit)) {
                 // push start, continue with start+1 (the reference pops start+1 first)
-                if (lane == 0) {
-                    st.node[sp] = start;
-                    st.mask[sp] = pm;
-                }
+                // slot sp of the stack VGPRs := {start, pm} (one compare + three selects)
+                const bool at = lane == sp;
+                stk_node = at ? start : stk_node;
+                stk_mlo = at ? (int)(uint32_t)pm : stk_mlo;
+                stk_mhi = at ? (int)(uint32_t)(pm >> 32) : stk_mhi;
                 sp++;
                 node = start + 1;
                 mask = pm;
-                descend = true;
-            } else if (level == 0) {
+                continue;
+            }
+            const int count = (int)(cl & 0xffffu);
+            if (level == 0) {
                 inst_next = start;
                 inst_end = start + count;
                 inst_mask = pm;
                 level = 1;
                 base = sp;
             } else {
-                const bool in = (pm & me) != 0;
-                ray3 tr = {lo_o, ld, wray.tmin, ltmax};
-                bool leaf_hit = false;
+                const bool in = (pm >> lane) & 1;
+                int leaf_hit = 0;
                 for (int i = start; i < start + count; i++) {
                     const f4* pr = S.sprims + 3 * i;
-                    const float4 a = ld4(pr), b = ld4(pr + 1), c = ld4(pr + 2);
-                    if (!in) continue;
-                    if (COUNT) wc.prim++;
+                    float4 pv[3];
+                    ld_uniform<3>(pr, pv);
+                    const float4 a = pv[0], b = pv[1], c = pv[2];
+                    if (COUNT && in && !(ANY && leaf_hit)) wc.prim++;
+                    if (COUNT && lane == 0) wc.wprim++;
                     float t;
                     vec4f ew;
                     bool h;
-                    if (kind == kind_triangles)
-                        h = tri_hit(tr, xyz(a), xyz(b), xyz(c), t, ew);
-                    else if (kind == kind_lines)
-                        h = line_hit(tr, xyz(a), xyz(b), b.w, c.x, t, ew);
-                    else
-                        h = point_hit(tr, xyz(a), b.x, t, ew);
-                    if (ANY && h) {
-                        leaf_hit = true;
-                        break;
+                    if (kind == kind_triangles) {
+                        float w1, w2;
+                        h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2);
+                        ew = {1 - w1 - w2, w1, w2, 0};
+                    } else {
+                        const ray3 lr = {co, cd, tmin, tmax};
+                        h = kind == kind_lines ? line_hit(lr, xyz(a), xyz(b), b.w, c.x, t, ew)
+                                               : point_hit(lr, xyz(a), b.x, t, ew);
                     }
-                    if (h) {
-                        tr.tmax = t;
-                        hr.slot = cur_slot;
-                        hr.ei = ibits(a.w);
-                        hr.ew = ew;
-                        hr.dist = t;
-                        leaf_hit = true;
+                    h = h && in;
+                    if (!ANY) {
+                        tmax = h ? t : tmax;
+                        hr.slot = h ? cur_slot : hr.slot;
+                        hr.ei = h ? ibits(a.w) : hr.ei;
+                        hr.ew = h ? ew : hr.ew;
+                        hr.dist = h ? t : hr.dist;
                     }
+                    leaf_hit |= h ? 1 : 0;
                 }
-                if (leaf_hit) hit = true;
-                if (ANY) {
-                    done |= ballot(leaf_hit);
-                    if (!(live & ~done)) return hit;
-                } else {
-                    // the reference sets tray.tmax = dist once the shape returns a hit;
-                    // nothing reads the world tmax before that, so updating it here is equivalent
-                    ltmax = tr.tmax;
-                    if (leaf_hit) wray.tmax = tr.tmax;
-                }
+                hit |= leaf_hit;
+                // any-hit lanes are finished; a NaN tmax fails every later slab test
+                done |= ballot(ANY ? leaf_hit : (leaf_hit && is_nan(tmax)));
+                if (ANY && !(live & ~done)) return hit;
             }
         }
-        if (descend) continue;
         // ---- next: the next instance of the current leaf, or pop ----
-        bool found = false;
-        while (!found) {
+        for (;;) {
             if (level == 1 && sp == base) {
                 if (inst_next < inst_end) {
                     // enter instance k: transform_ray_inverse (vmath.h:275-278), every lane
                     const int k = inst_next++;
                     const f4* ti = S.tinst + 4 * k;
-                    const float4 fx = ld4(ti), fy = ld4(ti + 1), fz = ld4(ti + 2), fo = ld4(ti + 3);
+                    float4 fr[4];
+                    ld_uniform<4>(ti, fr);
+                    const float4 fx = fr[0], fy = fr[1], fz = fr[2], fo = fr[3];
                     const frame3f f = {xyz(fx), xyz(fy), xyz(fz), xyz(fo)};
-                    lo_o = transform_point_inverse(f, wray.o);
-                    ld = transform_direction_inverse(f, wray.d);
-                    linvd = {1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z};
-                    ltmax = wray.tmax;
-                    const int4 sh = ld4(S.shapes + uniform(ibits(fx.w)));
-                    root = uniform(sh.x);
-                    kind = uniform(sh.y);
+                    co = transform_point_inverse(f, wo);
+                    cd = transform_direction_inverse(f, wd);
+                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    const uint32_t rk = (uint32_t)uniform(ibits(fo.w));
+                    root = (int)(rk & 0x3fffffffu);
+                    kind = (int)(rk >> 30);
+                    nbase = S.snodes + 2 * root;
                     cur_slot = k;
-                    node = 0;
+                    node = 0;  // the shape root, tested like any popped node
                     mask = inst_mask & ~done;
                     if (COUNT && (mask & me)) wc.inst++;
-                    found = mask != 0;
+                    if (mask) break;
                     continue;
                 }
                 level = 0;
+                nbase = S.tnodes;
+                co = wo;
+                cd = wd;
+                ci = wi;
             }
             if (sp == 0) return hit;
             sp--;
-            node = uniform(st.node[sp]);
-            mask = uniform64(st.mask[sp]) & ~done;
-            found = mask != 0;
+            node = __builtin_amdgcn_readlane(stk_node, sp);
+            const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp);
+            const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp);
+            mask = ((unsigned long long)mhi << 32 | mlo) & ~done;
+            if (mask) break;
         }
     }
 }

@@ -123,7 +123,7 @@ __device__ void flush_counters(unsigned long long* counters, const lane_state& L
     int n = COUNT ? 9 : 3;
     for (int k = 0; k < n; k++) {
         unsigned long long s = wave_sum(vals[k]);
-        if ((threadIdx.x & 63) == 0 && s) atomicAdd(counters + k, s);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + k, s);
     }
 }
 
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(dev_scene_view S, co
         }
     }
     unsigned long long s = wave_sum(k < n ? 1ull : 0ull);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(counters + cnt_rays, s);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + cnt_rays, s);
 }
 
 // tonemap (image.cpp:55-77): exposure 0, no filmic, gamma 1/2.2, truncating *255

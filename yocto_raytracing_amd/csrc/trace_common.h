@@ -20,10 +20,20 @@ struct ray3 {
 
 struct work_counts {
     unsigned long long box = 0, inst = 0, prim = 0, hits = 0, tex = 0;
+    unsigned long long wnode = 0, wprim = 0;  // packet walk: steps of the wave (counted in lane 0)
 };
 
 __device__ __forceinline__ float4 ld4(const f4* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ int4 ld4(const i4* p) { return *reinterpret_cast<const int4*>(p); }
+// a 16-byte record fetched whole, now: the empty asm consumes all four lanes at this
+// point, so the compiler can neither narrow the load to its xyz part nor sink a
+// separate load of .w into a later branch (which would put a second dependent memory
+// round trip on a traversal step)
+__device__ __forceinline__ float4 ld4_whole(const f4* p) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    return v;
+}
 __device__ __forceinline__ vec3f xyz(float4 v) { return {v.x, v.y, v.z}; }
 __device__ __forceinline__ int ibits(float f) { return __float_as_int(f); }
 __device__ __forceinline__ uint32_t ubits(float f) { return __float_as_uint(f); }
@@ -423,6 +433,13 @@ __device__ __forceinline__ ray3 camera_ray(const dev_camera& cam, int W, int H, 
     q.z = cam.oz + (u - 0.5f) * cam.w * cam.xz + (v - 0.5f) * cam.h * cam.yz - cam.focus * cam.zz;
     vec3f o = {cam.ox, cam.oy, cam.oz};
     return {o, normalize(q - o), ray_eps, flt_max};
+}
+
+// this wave's counter line (yrt_device.h: cnt_slots lines of cnt_count counters)
+__device__ __forceinline__ unsigned long long* counter_line(unsigned long long* counters) {
+    const unsigned wave = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
+                          (threadIdx.x >> 6);
+    return counters + (size_t)(wave % cnt_slots) * cnt_count;
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {

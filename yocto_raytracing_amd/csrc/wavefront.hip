@@ -35,6 +35,9 @@ namespace yrt {
 namespace {
 
 constexpr int WF_BLOCK = 256;
+#ifndef YRT_EXP_SHADOW_LDS
+#define YRT_EXP_SHADOW_LDS 0  // experiment knob: dynamic LDS per shadow block (occupancy cap)
+#endif
 constexpr int MAX_LEVELS = 16;
 constexpr int TILE = 8;  // pixel tiles of 8x8 in the sample enumeration
 
@@ -80,8 +83,34 @@ __device__ __forceinline__ bool pixel_of(const dev_render_args& A, int tiles_x, 
 
 template <bool COUNT>
 __device__ __forceinline__ void flush(unsigned long long* counters, int idx, unsigned long long v) {
+#ifdef YRT_EXP_NOCOUNT  // diagnostic: no per-wave counter atomics in the timed kernels
+    if (!COUNT) return;
+#endif
     unsigned long long s = wave_sum(v);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(counters + idx, s);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + idx, s);
+}
+
+// the timed kernels' counters: wave sums combined per block in LDS, then ONE device
+// atomic per counter per block into the block's counter line (a per-wave atomic
+// costs ~4x as many fabric atomics; the c4 shadow pass has 1.5 M blocks)
+template <int N>
+__device__ __forceinline__ void flush_block(unsigned long long* counters, const int (&idx)[N],
+                                            const unsigned long long (&v)[N]) {
+    __shared__ unsigned long long part[WF_BLOCK / 64][N];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const unsigned long long s = wave_sum(v[k]);
+        if ((threadIdx.x & 63) == 0) part[w][k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < N) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int q = 0; q < WF_BLOCK / 64; q++) t += part[q][threadIdx.x];
+        const unsigned b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        if (t) atomicAdd(counters + (size_t)(b % cnt_slots) * cnt_count + idx[threadIdx.x], t);
+    }
 }
 
 __device__ __forceinline__ void flush_work(unsigned long long* counters, const work_counts& wc) {
@@ -90,6 +119,8 @@ __device__ __forceinline__ void flush_work(unsigned long long* counters, const w
     flush<true>(counters, cnt_prim_tests, wc.prim);
     flush<true>(counters, cnt_shaded_hits, wc.hits);
     flush<true>(counters, cnt_tex_lookups, wc.tex);
+    flush<true>(counters, cnt_wave_node_visits, wc.wnode);
+    flush<true>(counters, cnt_wave_prim_visits, wc.wprim);
 }
 
 __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool hit, const surface& sf) {
@@ -107,19 +138,18 @@ __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool
 // (trace_common.h). Both are called in wave-uniform control flow.
 template <bool ANY, bool COUNT, bool PACKET, typename SE>
 struct tracer {
-    static constexpr int WAVES = WF_BLOCK / 64;
     SE* lane_stk;
-    wave_stack wst;
     __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
                                           work_counts& wc) {
-        if (PACKET) return packet_trace<ANY, COUNT>(S, ray, valid, hr, wst, wc);
+        if (PACKET) return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
         if (!valid) return false;
         if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
         return traverse<false, COUNT, WF_BLOCK>(S, ray, hr, lane_stk, wc);
     }
 };
 
-// LDS for either schedule: per-lane columns, or one {node, mask} stack per wave
+// LDS for either schedule: per-lane stack columns; the packet walk keeps its stack
+// in VGPR lanes and needs none
 template <bool PACKET, typename SE>
 struct traversal_lds;
 template <typename SE>
@@ -128,21 +158,16 @@ struct traversal_lds<false, SE> {
 };
 template <typename SE>
 struct traversal_lds<true, SE> {
-    unsigned long long mask[WF_BLOCK / 64][traversal_stack_cap];
-    int node[WF_BLOCK / 64][traversal_stack_cap];
+    int unused;
 };
 
 template <bool ANY, bool COUNT, bool PACKET, typename SE>
 __device__ __forceinline__ tracer<ANY, COUNT, PACKET, SE> make_tracer(traversal_lds<PACKET, SE>& L) {
     tracer<ANY, COUNT, PACKET, SE> t;
-    if constexpr (PACKET) {
-        const int w = threadIdx.x / 64;
+    if constexpr (PACKET)
         t.lane_stk = nullptr;
-        t.wst = {L.node[w], L.mask[w]};
-    } else {
+    else
         t.lane_stk = L.lane + threadIdx.x;
-        t.wst = {nullptr, nullptr};
-    }
     return t;
 }
 
@@ -179,8 +204,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_primary(dev_scene_view S, dev_rend
         }
         store_surface(B, idx, hit, sf);
     }
-    flush<false>(counters, cnt_rays, valid ? 1 : 0);
-    flush<false>(counters, cnt_samples, valid ? 1 : 0);
+    flush_block<2>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
     if (COUNT) flush_work(counters, wc);
 }
 
@@ -215,7 +239,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_bounce(dev_scene_view S, int level
             store_surface(B, idx, hit, sf);
         }
     }
-    flush<false>(counters, cnt_rays, rays);
+    flush_block<1>(counters, {cnt_rays}, {rays});
     if (COUNT) flush_work(counters, wc);
 }
 
@@ -254,13 +278,14 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shadow(dev_scene_view S, int level
         const bool occ = T.trace(S, sr, valid, hr, wc);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
     }
-    flush<false>(counters, cnt_rays, rays);
-    flush<false>(counters, cnt_shadow_rays, rays);
+    // shadow rays are counted once, here; yrt_last_stats reports rays = cnt_rays + this
+    flush_block<1>(counters, {cnt_shadow_rays}, {rays});
     if (COUNT) {
         flush_work(counters, wc);
         flush<true>(counters, cnt_shadow_box_tests, wc.box);
         flush<true>(counters, cnt_shadow_inst_entries, wc.inst);
         flush<true>(counters, cnt_shadow_prim_tests, wc.prim);
+        flush<true>(counters, cnt_shadow_wave_node_visits, wc.wnode);
     }
 }
 
@@ -508,7 +533,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid : grid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
-                hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE>), sg, dim3(WF_BLOCK), 0, stream, ds.view, level, nsamp, B,
+                hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE>), sg, dim3(WF_BLOCK), YRT_EXP_SHADOW_LDS, stream, ds.view, level, nsamp, B,
                                    counters);
                 T.end(t, stream);
             }

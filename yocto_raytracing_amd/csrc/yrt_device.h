@@ -4,7 +4,8 @@
 // Everything is 16-byte records so each fetch is one global_load_dwordx4:
 //   tnodes  2 x f4 per instance-BVH node  {min.xyz, start} {max.xyz, count|leaf<<31}
 //   tinst   4 x f4 per instance-BVH leaf slot (instances permuted to leaf order)
-//           {frame.x, shape} {frame.y, instance id} {frame.z, material} {frame.o, -}
+//           {frame.x, shape} {frame.y, instance id} {frame.z, material}
+//           {frame.o, shape root node | kind << 30}
 //   snodes  2 x f4 per shape-BVH node, all shapes concatenated, child/leaf indices absolute
 //   sprims  3 x f4 per shape-BVH leaf slot (primitives permuted to leaf order)
 //           triangle {v0, ei} {v1-v0, -} {v2-v0, -}   (the reference's e1/e2, scene.cpp:232-233)
@@ -96,7 +97,19 @@ enum counter_index {
     cnt_shadow_box_tests = 10,
     cnt_shadow_inst_entries = 11,
     cnt_shadow_prim_tests = 12,
+    // the packet walk: node records / primitive records fetched per WAVE (one per
+    // step whatever the number of active lanes): lanes-per-step = box_tests / this
+    cnt_wave_node_visits = 13,
+    cnt_wave_prim_visits = 14,
+    cnt_shadow_wave_node_visits = 15,
     cnt_count = 16
 };
+
+// The counters live in cnt_slots lines of cnt_count u64 (128 bytes each); a wave adds
+// its sums into the line picked by its global wave index and the host adds the lines.
+// One shared address for every wave serialises the device-scope atomics: with a
+// single line the per-wave counter flush alone cost ~30 ms of a 78 ms c4 shadow pass.
+constexpr int cnt_slots = 1024;
+static_assert(cnt_count * 8 == 128, "one counter line = one 128-byte cache line");
 
 }  // namespace yrt
