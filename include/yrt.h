@@ -182,6 +182,10 @@ int yrt_trace_first(yrt_scene* ds, const float* rays, int n, unsigned char* hit,
                     float* ew, float* dist, int mem, void* stream);
 /* batch intersect_any (src/scene.cpp:489-493) */
 int yrt_trace_any(yrt_scene* ds, const float* rays, int n, unsigned char* hit, int mem, void* stream);
+/* walks used by yrt_trace_first/any on this handle (identical results): YRT_ALGO_WAVEFRONT
+ * (default) = the render path's wave-coherent closest-hit walk and 4-wide any-hit walk;
+ * YRT_ALGO_MEGAKERNEL / YRT_ALGO_WAVEFRONT_LANE = one independent walk per lane */
+int yrt_scene_set_trace_algorithm(yrt_scene* ds, int algorithm);
 /* counters of the last render/trace call on this handle (synchronises the stream) */
 int yrt_last_stats(yrt_scene* ds, yrt_stats* stats);
 /* per-phase GPU times of the last yrt_render with p->timing = 1 (synchronises) */

@@ -176,6 +176,10 @@ class DeviceScene:
         except Exception:
             pass
 
+    def set_trace_algorithm(self, algorithm: str) -> None:
+        """walks used by intersect_first/intersect_any on this scene (identical results)"""
+        check(N.lib.yrt_scene_set_trace_algorithm(self._h, ALGORITHMS[algorithm]), "set_trace_algorithm")
+
     @property
     def device_bytes(self) -> int:
         return int(N.lib.yrt_scene_device_bytes(self._h))

@@ -100,6 +100,7 @@ _sig = {
     "yrt_render": (C.c_int, [_vp, C.POINTER(RenderParams), _vp, C.c_int, _vp]),
     "yrt_trace_first": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp]),
     "yrt_trace_any": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int, _vp]),
+    "yrt_scene_set_trace_algorithm": (C.c_int, [_vp, C.c_int]),
     "yrt_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "yrt_last_timings": (C.c_int, [_vp, C.POINTER(Timings)]),
     "yrt_tonemap": (C.c_int, [_vp, C.c_int, _vp, C.c_int, _vp]),

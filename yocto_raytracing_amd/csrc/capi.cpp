@@ -22,6 +22,7 @@ struct yrt_scene {
     void* scratch = nullptr;                 // device staging for host-memory calls
     size_t scratch_bytes = 0;
     hipStream_t last_stream = nullptr;
+    int trace_algorithm = YRT_ALGO_WAVEFRONT;  // walks used by yrt_trace_first/any
 };
 
 namespace {
@@ -362,6 +363,12 @@ int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out) {
     });
 }
 
+int yrt_scene_set_trace_algorithm(yrt_scene* s, int algorithm) {
+    if (!s || algorithm < YRT_ALGO_WAVEFRONT || algorithm > YRT_ALGO_WAVEFRONT_LANE) return YRT_ERR_INVALID_ARG;
+    s->trace_algorithm = algorithm;
+    return YRT_OK;
+}
+
 size_t yrt_scene_device_bytes(const yrt_scene* s) { return s && s->ds ? s->ds->arena_bytes : 0; }
 
 void yrt_scene_free(yrt_scene* s) {
@@ -449,7 +456,8 @@ static int trace_impl(yrt_scene* s, const float* rays, int n, int any, unsigned 
         s->last_stream = st;
         if (n == 0) return YRT_OK;
         if (mem == YRT_MEM_DEVICE) {
-            hip_check(yrt::launch_trace(*s->ds, rays, n, any, hit, inst, ei, ew, dist, s->counters, st), "trace launch");
+            hip_check(yrt::launch_trace(*s->ds, rays, n, any, hit, inst, ei, ew, dist, s->counters,
+                                              s->trace_algorithm == YRT_ALGO_WAVEFRONT, st), "trace launch");
             return YRT_OK;
         }
         size_t rb = (size_t)n * 8 * 4, hb = ((size_t)n + 255) & ~(size_t)255, ib = (size_t)n * 4, eb = (size_t)n * 16;
@@ -461,7 +469,8 @@ static int trace_impl(yrt_scene* s, const float* rays, int n, int any, unsigned 
         float* d_dist = (float*)(base + rb + hb + 2 * ib);
         float* d_ew = (float*)(base + rb + hb + 3 * ib);
         hip_check(hipMemcpyAsync(d_rays, rays, rb, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
-        hip_check(yrt::launch_trace(*s->ds, d_rays, n, any, d_hit, d_inst, d_ei, d_ew, d_dist, s->counters, st),
+        hip_check(yrt::launch_trace(*s->ds, d_rays, n, any, d_hit, d_inst, d_ei, d_ew, d_dist, s->counters,
+                                    s->trace_algorithm == YRT_ALGO_WAVEFRONT, st),
                   "trace launch");
         hip_check(hipMemcpyAsync(hit, d_hit, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
         if (!any) {

@@ -56,6 +56,67 @@ struct arena_builder {
     }
 };
 
+// 4-wide collapse of a binary BVH for the any-hit walk: a wide node
+// holds the children of a binary node X with every INNER child replaced by its two
+// children, so one visit tests up to four boxes two levels below X. The boxes, the
+// leaves and the primitive order are the reference's; only the inner boxes that are
+// skipped are not tested. For an any-hit query that changes nothing: a box test is
+// monotone in the box (a box inside another passes only if the outer one passes,
+// NaN slabs included, trace_common.h box_hit), so every leaf reached here is one the
+// reference reaches too, and the answer of intersect_any does not depend on the order
+// in which the leaves are tested.
+// Record (8 x f4, 128 bytes): lo.x[4] lo.y[4] lo.z[4] hi.x[4] hi.y[4] hi.z[4], then
+// per slot the reference (wide node index, or first leaf slot + `leaf_base`) and the
+// info (0 empty slot, 1 inner, count | leaf_bit for a leaf).
+struct wide_builder {
+    std::vector<f4>& out;
+    int max_depth = 0;
+
+    int emit(const bvh_tree& t, int x, uint32_t leaf_base, int depth) {
+        max_depth = std::max(max_depth, depth);
+        std::vector<int> slots;
+        const bvh_node& n = t.nodes[x];
+        if (n.isleaf) {
+            slots.push_back(x);
+        } else {
+            for (int c : {(int)n.start + 1, (int)n.start}) {  // the reference visits start+1 first
+                const bvh_node& cn = t.nodes[c];
+                if (cn.isleaf) {
+                    slots.push_back(c);
+                } else {
+                    slots.push_back((int)cn.start + 1);
+                    slots.push_back((int)cn.start);
+                }
+            }
+        }
+        const int me = (int)out.size() / 8;
+        out.resize(out.size() + 8, f4{0, 0, 0, 0});
+        float v[6][4];
+        int ref[4] = {0, 0, 0, 0}, info[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; k++) {
+            if (k >= (int)slots.size()) {  // empty slot: an inverted box, and info 0
+                for (int a = 0; a < 3; a++) v[a][k] = INFINITY, v[3 + a][k] = -INFINITY;
+                continue;
+            }
+            const bvh_node& s = t.nodes[slots[k]];
+            v[0][k] = s.bbox.min.x, v[1][k] = s.bbox.min.y, v[2][k] = s.bbox.min.z;
+            v[3][k] = s.bbox.max.x, v[4][k] = s.bbox.max.y, v[5][k] = s.bbox.max.z;
+            if (s.isleaf) {
+                ref[k] = (int)(s.start + leaf_base);
+                info[k] = (int)((uint32_t)s.count | leaf_bit);
+            } else {
+                info[k] = 1;
+            }
+        }
+        for (int k = 0; k < 4; k++)
+            if (info[k] == 1) ref[k] = emit(t, slots[k], leaf_base, depth + 1);
+        for (int a = 0; a < 6; a++) out[(size_t)me * 8 + a] = {v[a][0], v[a][1], v[a][2], v[a][3]};
+        out[(size_t)me * 8 + 6] = {as_float(ref[0]), as_float(ref[1]), as_float(ref[2]), as_float(ref[3])};
+        out[(size_t)me * 8 + 7] = {as_float(info[0]), as_float(info[1]), as_float(info[2]), as_float(info[3])};
+        return me;
+    }
+};
+
 }  // namespace
 
 dev_camera make_dev_camera(const camera& c) {
@@ -112,6 +173,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     std::vector<f4> snodes, sprims, vpos, vnorm;
     std::vector<f2> vuv;
     std::vector<i4> shapes, elems;
+    std::vector<uint32_t> shape_prim_base;
     for (size_t si = 0; si < scn.shapes.size(); si++) {
         const shape& s = scn.shapes[si];
         int kinds = (!s.triangles.empty()) + (!s.lines.empty()) + (!s.points.empty());
@@ -168,11 +230,35 @@ device_scene* device_scene_create(const scene& scn, int device) {
             vuv.push_back({t.x, t.y});
         }
         shapes.push_back({node_base, kind, elem_base, vert_base});
+        shape_prim_base.push_back((uint32_t)prim_base);
         ds->max_shape_nodes = std::max(ds->max_shape_nodes, s.bvh.nodes.size());
     }
 
+    // ---- 4-wide collapse for the any-hit walk: instance level first, then shapes ----
+    std::vector<f4> wnodes;
+    wide_builder wb{wnodes};
+    const int wtop_root = wb.emit(scn.bvh, 0, 0, 1);
+    const int wtop_depth = wb.max_depth;
+    std::vector<int> wshape_root(scn.shapes.size());
+    int wshape_depth = 0;
+    for (size_t si = 0; si < scn.shapes.size(); si++) {
+        wb.max_depth = 0;
+        wshape_root[si] = scn.shapes[si].bvh.nodes.empty() ? -1 : wb.emit(scn.shapes[si].bvh, 0, shape_prim_base[si], 1);
+        wshape_depth = std::max(wshape_depth, wb.max_depth);
+    }
+    // instances of an empty shape enter a wide node with no slots
+    const int wempty = (int)wnodes.size() / 8;
+    wnodes.resize(wnodes.size() + 8, f4{0, 0, 0, 0});
+    for (int a = 0; a < 3; a++) wnodes[(size_t)wempty * 8 + a] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    for (int a = 3; a < 6; a++) wnodes[(size_t)wempty * 8 + a] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (auto& r : wshape_root)
+        if (r < 0) r = wempty;
+    // the wide walk pushes at most three siblings per visit
+    ds->wide_ok = 3 * (wtop_depth + wshape_depth) + 2 <= 64;
+
     // ---- instance level: nodes + instances permuted into leaf order ----
     std::vector<f4> tnodes, tinst;
+    std::vector<int> tinst_id;
     for (auto& n : scn.bvh.nodes) {
         tnodes.push_back(node_lo(n, n.start));
         tnodes.push_back(node_hi(n));
@@ -183,7 +269,10 @@ device_scene* device_scene_create(const scene& scn, int device) {
             throw std::runtime_error("instance " + ist.name + " has no material");
         const frame3f& f = ist.frame;
         tinst.push_back({f.x.x, f.x.y, f.x.z, as_float(ist.shp)});
-        tinst.push_back({f.y.x, f.y.y, f.y.z, as_float(ii)});
+        // .w: the shape's wide root | kind << 30 (the any-hit walk's entry)
+        const int wr = wshape_root[ist.shp];
+        tinst.push_back({f.y.x, f.y.y, f.y.z, as_float((int)((uint32_t)wr | ((uint32_t)shapes[ist.shp].y << 30)))});
+        tinst_id.push_back(ii);
         tinst.push_back({f.z.x, f.z.y, f.z.z, as_float(ist.mat)});
         // .w of the last row: the shape's root node and primitive kind, so a traversal
         // entering the instance needs no dependent fetch of the shape record
@@ -252,6 +341,8 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_texels = ab.add(texels.data(), texels.size() * sizeof(uint32_t));
     size_t o_texinfo = ab.add(texinfo.data(), texinfo.size() * sizeof(i4));
     size_t o_srgb = ab.add(srgb.data(), srgb.size() * sizeof(float));
+    size_t o_wnodes = ab.add(wnodes.data(), wnodes.size() * sizeof(f4));
+    size_t o_tinst_id = ab.add(tinst_id.data(), tinst_id.size() * sizeof(int));
 
     try {
         check(hipSetDevice(device), "hipSetDevice");
@@ -281,6 +372,10 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.texels = (const uint32_t*)(base + o_texels);
     v.texinfo = (const i4*)(base + o_texinfo);
     v.srgb = (const float*)(base + o_srgb);
+    v.wnodes = (const f4*)(base + o_wnodes);
+    v.tinst_id = (const int*)(base + o_tinst_id);
+    v.wtop_root = wtop_root;
+    v.wide = ds->wide_ok ? 1 : 0;
     v.nlights = (int)lights.size() / 6;
     ds->nlights = v.nlights;
     v.ntnodes = (int)tnodes.size() / 2;

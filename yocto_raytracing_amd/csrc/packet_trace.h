@@ -73,18 +73,66 @@ __device__ __forceinline__ void ld_uniform(const f4* p, float4 (&out)[N]) {
     // their lanes (no narrowed loads, no .w reload sunk into a later branch)
 #pragma unroll
     for (int k = 0; k < N; k++) out[k] = *reinterpret_cast<const float4*>(p + k);
-    if constexpr (N == 2)
-        asm volatile("" : "+v"(out[0].x), "+v"(out[0].y), "+v"(out[0].z), "+v"(out[0].w), "+v"(out[1].x),
-                     "+v"(out[1].y), "+v"(out[1].z), "+v"(out[1].w));
-    if constexpr (N == 3)
-        asm volatile("" : "+v"(out[0].x), "+v"(out[0].y), "+v"(out[0].z), "+v"(out[0].w), "+v"(out[1].x),
-                     "+v"(out[1].y), "+v"(out[1].z), "+v"(out[1].w), "+v"(out[2].x), "+v"(out[2].y),
-                     "+v"(out[2].z), "+v"(out[2].w));
-    if constexpr (N == 4)
-        asm volatile("" : "+v"(out[0].x), "+v"(out[0].y), "+v"(out[0].z), "+v"(out[0].w), "+v"(out[1].x),
-                     "+v"(out[1].y), "+v"(out[1].z), "+v"(out[1].w), "+v"(out[2].x), "+v"(out[2].y),
-                     "+v"(out[2].z), "+v"(out[2].w), "+v"(out[3].x), "+v"(out[3].y), "+v"(out[3].z),
-                     "+v"(out[3].w));
+#pragma unroll
+    for (int k = 0; k < N; k += 2) {
+        if (k + 1 < N)
+            asm volatile("" : "+v"(out[k].x), "+v"(out[k].y), "+v"(out[k].z), "+v"(out[k].w), "+v"(out[k + 1].x),
+                         "+v"(out[k + 1].y), "+v"(out[k + 1].z), "+v"(out[k + 1].w));
+        else
+            asm volatile("" : "+v"(out[k].x), "+v"(out[k].y), "+v"(out[k].z), "+v"(out[k].w));
+    }
+#endif
+}
+
+// N consecutive 16-byte records at a wave-uniform address through the scalar data
+// cache into SGPRs (s_load_dwordx4/x8/x16; the scene is read-only for the whole
+// launch). The VALU reads them as scalar operands; nothing occupies the vector memory
+// pipe, which a 64-lane load of one shared address would (1 KiB returned per record).
+typedef int sgpr4 __attribute__((ext_vector_type(4)));
+typedef int sgpr8 __attribute__((ext_vector_type(8)));
+typedef int sgpr16 __attribute__((ext_vector_type(16)));
+template <typename V>
+__device__ __forceinline__ float4 rec_of(const V& v, int k) {
+    return {__int_as_float(v[4 * k]), __int_as_float(v[4 * k + 1]), __int_as_float(v[4 * k + 2]),
+            __int_as_float(v[4 * k + 3])};
+}
+template <int N>
+__device__ __forceinline__ void ld_scalar(const f4* p, float4 (&out)[N]) {
+    static_assert(N == 2 || N == 3 || N == 4 || N == 8, "record count");
+    if constexpr (N == 2) {
+        sgpr8 a;
+        asm volatile("s_load_dwordx8 %0, %1, 0x0\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1);
+    } else if constexpr (N == 3) {
+        sgpr8 a;
+        sgpr4 b;
+        asm volatile("s_load_dwordx8 %0, %2, 0x0\n s_load_dwordx4 %1, %2, 0x20\n s_waitcnt lgkmcnt(0)"
+                     : "=s"(a), "=s"(b)
+                     : "s"(p));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(b, 0);
+    } else if constexpr (N == 4) {
+        sgpr16 a;
+        asm volatile("s_load_dwordx16 %0, %1, 0x0\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+    } else {
+        sgpr16 a, b;
+        asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx16 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
+                     : "=s"(a), "=s"(b)
+                     : "s"(p));
+#pragma unroll
+        for (int k = 0; k < 4; k++) out[k] = rec_of(a, k), out[4 + k] = rec_of(b, k);
+    }
+}
+
+#ifndef YRT_SCALAR_LOADS
+#define YRT_SCALAR_LOADS 1  // 0: 64-lane vector loads of the shared records (A/B)
+#endif
+template <int N>
+__device__ __forceinline__ void ld_records(const f4* p, float4 (&out)[N]) {
+#if YRT_SCALAR_LOADS
+    ld_scalar<N>(p, out);
+#else
+    ld_uniform<N>(p, out);
 #endif
 }
 
@@ -132,7 +180,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
         // ---- every lane of `mask` tests `node` with its own ray ----
         const f4* nb = nbase + 2 * node;
         float4 rec[2];
-        ld_uniform<2>(nb, rec);
+        ld_records<2>(nb, rec);
         const float4 lo = rec[0], hi = rec[1];
         if (COUNT && (mask & me)) wc.box++;
         if (COUNT && lane == 0) wc.wnode++;
@@ -188,7 +236,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                 for (int i = start; i < start + count; i++) {
                     const f4* pr = S.sprims + 3 * i;
                     float4 pv[3];
-                    ld_uniform<3>(pr, pv);
+                    ld_records<3>(pr, pv);
                     const float4 a = pv[0], b = pv[1], c = pv[2];
                     if (COUNT && in && !(ANY && leaf_hit)) wc.prim++;
                     if (COUNT && lane == 0) wc.wprim++;
@@ -228,7 +276,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     const int k = inst_next++;
                     const f4* ti = S.tinst + 4 * k;
                     float4 fr[4];
-                    ld_uniform<4>(ti, fr);
+                    ld_records<4>(ti, fr);
                     const float4 fx = fr[0], fy = fr[1], fz = fr[2], fo = fr[3];
                     const frame3f f = {xyz(fx), xyz(fy), xyz(fz), xyz(fo)};
                     co = transform_point_inverse(f, wo);
@@ -254,6 +302,135 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
             if (sp == 0) return hit;
             sp--;
             node = __builtin_amdgcn_readlane(stk_node, sp);
+            const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp);
+            const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp);
+            mask = ((unsigned long long)mhi << 32 | mlo) & ~done;
+            if (mask) break;
+        }
+    }
+}
+
+
+// ---- any-hit on the 4-wide collapse (device_scene.cpp wide_builder) ----
+// The same packet discipline (SGPR control, VGPR-lane stack, lane masks), over wide
+// nodes: a visit fetches one 128-byte record and every lane of the mask tests the
+// four child boxes with its own ray; the passing children are pushed (the first one
+// is entered directly). Leaves are the reference's: instance leaves enter their
+// instances in slot order, shape leaves test their primitives. A lane leaves the
+// walk at its first hit. Results equal intersect_any's (see wide_builder for why the
+// skipped inner boxes and the order do not matter); the instrumented (COUNT) kernels
+// use the binary walk instead, so work counts stay the reference's.
+__device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, const ray3& wray, bool valid) {
+    const int lane = __lane_id();
+    const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
+    if (!live) return false;
+    const vec3f wo = wray.o, wd = wray.d;
+    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    const float tmin = wray.tmin, tmax = wray.tmax;
+    vec3f co = wo, cd = wd, ci = wi;
+    int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
+    unsigned long long done = 0, inst_mask = 0;
+    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
+    // the current item: a wide node (info 1) or a leaf (info = count | leaf_bit)
+    int ref = S.wtop_root;
+    uint32_t info = 1;
+    unsigned long long mask = live;
+    for (;;) {
+        if (!(info & leaf_bit)) {
+            float4 r[8];
+            ld_records<8>(S.wnodes + 8 * ref, r);
+            const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
+                        lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
+                        hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
+            const int rf[4] = {ibits(r[6].x), ibits(r[6].y), ibits(r[6].z), ibits(r[6].w)};
+            const int in[4] = {ibits(r[7].x), ibits(r[7].y), ibits(r[7].z), ibits(r[7].w)};
+            unsigned long long m[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float tn;
+                m[k] = ballot(in[k] != 0 && box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)) &
+                       mask;
+            }
+            int first = -1;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (!m[k]) continue;
+                if (first < 0) {
+                    first = k;
+                    continue;
+                }
+                const bool at = lane == sp;
+                stk_ref = at ? rf[k] : stk_ref;
+                stk_info = at ? in[k] : stk_info;
+                stk_mlo = at ? (int)(uint32_t)m[k] : stk_mlo;
+                stk_mhi = at ? (int)(uint32_t)(m[k] >> 32) : stk_mhi;
+                sp++;
+            }
+            if (first >= 0) {
+                const int rsel = first == 0 ? rf[0] : first == 1 ? rf[1] : first == 2 ? rf[2] : rf[3];
+                const int isel = first == 0 ? in[0] : first == 1 ? in[1] : first == 2 ? in[2] : in[3];
+                ref = uniform(rsel);
+                info = (uint32_t)uniform(isel);
+                mask = m[first];
+                continue;
+            }
+        } else if (level == 0) {
+            inst_next = ref;
+            inst_end = ref + (int)(info & 0xffffu);
+            inst_mask = mask;
+            level = 1;
+            base = sp;
+        } else {
+            const bool inl = (mask >> lane) & 1;
+            int leaf_hit = 0;
+            const int count = (int)(info & 0xffffu);
+            for (int i = ref; i < ref + count; i++) {
+                float4 pv[3];
+                ld_records<3>(S.sprims + 3 * i, pv);
+                float t;
+                bool h;
+                if (kind == kind_triangles) {
+                    float w1, w2;
+                    h = tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2);
+                } else {
+                    vec4f ew;
+                    const ray3 lr = {co, cd, tmin, tmax};
+                    h = kind == kind_lines ? line_hit(lr, xyz(pv[0]), xyz(pv[1]), pv[1].w, pv[2].x, t, ew)
+                                           : point_hit(lr, xyz(pv[0]), pv[1].x, t, ew);
+                }
+                leaf_hit |= (h && inl) ? 1 : 0;
+            }
+            done |= ballot(leaf_hit != 0);
+            if (!(live & ~done)) return (done >> lane) & 1;
+        }
+        // ---- next: the next instance of the current leaf, or pop ----
+        for (;;) {
+            if (level == 1 && sp == base) {
+                if (inst_next < inst_end) {
+                    const int k = inst_next++;
+                    float4 fr[4];
+                    ld_records<4>(S.tinst + 4 * k, fr);
+                    const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
+                    co = transform_point_inverse(f, wo);
+                    cd = transform_direction_inverse(f, wd);
+                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
+                    ref = (int)(rk & 0x3fffffffu);
+                    kind = (int)(rk >> 30);
+                    info = 1;
+                    mask = inst_mask & ~done;
+                    if (mask) break;
+                    continue;
+                }
+                level = 0;
+                co = wo;
+                cd = wd;
+                ci = wi;
+            }
+            if (sp == 0) return (done >> lane) & 1;
+            sp--;
+            ref = __builtin_amdgcn_readlane(stk_ref, sp);
+            info = (uint32_t)__builtin_amdgcn_readlane(stk_info, sp);
             const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp);
             const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp);
             mask = ((unsigned long long)mhi << 32 | mlo) & ~done;

@@ -9,6 +9,7 @@
 // are summed in the reference's jj-major / ii-minor order.
 #include <hip/hip_runtime.h>
 
+#include "packet_trace.h"
 #include "trace_common.h"
 #include "yrt_render.h"
 
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(dev_scene_view S, co
         hit[k] = h ? 1 : 0;
         if (!ANY) {
             // intersect_first returns a default record on a miss (scene.cpp:485-486)
-            inst[k] = h ? ibits(S.tinst[4 * hr.slot + 1].w) : -1;
+            inst[k] = h ? S.tinst_id[hr.slot] : -1;
             eis[k] = h ? hr.ei : -1;
             ews[4 * k + 0] = h ? hr.ew.x : 0;
             ews[4 * k + 1] = h ? hr.ew.y : 0;
@@ -191,6 +192,43 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(dev_scene_view S, co
         }
     }
     unsigned long long s = wave_sum(k < n ? 1ull : 0ull);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + cnt_rays, s);
+}
+
+// the same queries through the render path's walks: the wave-coherent closest-hit walk
+// and the 4-wide any-hit walk (packet_trace.h); every lane reaches the walk
+template <bool ANY>
+__global__ __launch_bounds__(TRACE_BLOCK) void trace_packet_kernel(dev_scene_view S, const float* __restrict__ rays,
+                                                                   int n, unsigned char* hit, int* inst, int* eis,
+                                                                   float* ews, float* dists,
+                                                                   unsigned long long* counters) {
+    const int k = blockIdx.x * TRACE_BLOCK + threadIdx.x;
+    const bool valid = k < n;
+    ray3 ray = {{0, 0, 0}, {0, 0, 1}, 0, 0};
+    if (valid) {
+        const float* r = rays + (size_t)k * 8;
+        ray = {{r[0], r[1], r[2]}, {r[3], r[4], r[5]}, r[6], r[7]};
+    }
+    hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
+    work_counts wc;
+    bool h;
+    if (ANY)
+        h = S.wide ? packet_occluded_wide(S, ray, valid) : packet_trace<true, false>(S, ray, valid, hr, wc);
+    else
+        h = packet_trace<false, false>(S, ray, valid, hr, wc);
+    if (valid) {
+        hit[k] = h ? 1 : 0;
+        if (!ANY) {
+            inst[k] = h ? S.tinst_id[hr.slot] : -1;
+            eis[k] = h ? hr.ei : -1;
+            ews[4 * k + 0] = h ? hr.ew.x : 0;
+            ews[4 * k + 1] = h ? hr.ew.y : 0;
+            ews[4 * k + 2] = h ? hr.ew.z : 0;
+            ews[4 * k + 3] = h ? hr.ew.w : 0;
+            dists[k] = h ? hr.dist : 0;
+        }
+    }
+    unsigned long long s = wave_sum(valid ? 1ull : 0ull);
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + cnt_rays, s);
 }
 
@@ -224,9 +262,19 @@ hipError_t launch_render(device_scene& ds, const dev_render_args& args, void* ou
 }
 
 hipError_t launch_trace(const device_scene& ds, const float* rays, int n, int any, unsigned char* hit, int* inst,
-                        int* ei, float* ew, float* dist, unsigned long long* counters, hipStream_t stream) {
+                        int* ei, float* ew, float* dist, unsigned long long* counters, bool packet,
+                        hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     dim3 grid((n + TRACE_BLOCK - 1) / TRACE_BLOCK);
+    if (packet) {
+        if (any)
+            hipLaunchKernelGGL(trace_packet_kernel<true>, grid, dim3(TRACE_BLOCK), 0, stream, ds.view, rays, n, hit,
+                               inst, ei, ew, dist, counters);
+        else
+            hipLaunchKernelGGL(trace_packet_kernel<false>, grid, dim3(TRACE_BLOCK), 0, stream, ds.view, rays, n, hit,
+                               inst, ei, ew, dist, counters);
+        return hipGetLastError();
+    }
     if (any)
         hipLaunchKernelGGL(trace_kernel<true>, grid, dim3(TRACE_BLOCK), 0, stream, ds.view, rays, n, hit, inst, ei,
                            ew, dist, counters);

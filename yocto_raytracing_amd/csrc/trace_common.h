@@ -47,10 +47,10 @@ __device__ __forceinline__ uint32_t ubits(float f) { return __float_as_uint(f); 
 // final <= cannot see. Callers guarantee non-NaN seeds (a NaN seed fails every test
 // in the reference, and the traversals return "no hit" up front for it).
 // The per-axis swap on invd < 0 stays a select: it must not drop NaNs.
-__device__ __forceinline__ bool box_hit(vec3f o, vec3f invd, float tmin_r, float tmax_r, float4 lo, float4 hi,
-                                        float& tnear) {
-    float t0x = (lo.x - o.x) * invd.x, t0y = (lo.y - o.y) * invd.y, t0z = (lo.z - o.z) * invd.z;
-    float t1x = (hi.x - o.x) * invd.x, t1y = (hi.y - o.y) * invd.y, t1z = (hi.z - o.z) * invd.z;
+__device__ __forceinline__ bool box_hit6(vec3f o, vec3f invd, float tmin_r, float tmax_r, float lx, float ly,
+                                         float lz, float hx, float hy, float hz, float& tnear) {
+    float t0x = (lx - o.x) * invd.x, t0y = (ly - o.y) * invd.y, t0z = (lz - o.z) * invd.z;
+    float t1x = (hx - o.x) * invd.x, t1y = (hy - o.y) * invd.y, t1z = (hz - o.z) * invd.z;
     if (invd.x < 0) { float t = t0x; t0x = t1x; t1x = t; }
     if (invd.y < 0) { float t = t0y; t0y = t1y; t1y = t; }
     if (invd.z < 0) { float t = t0z; t0z = t1z; t1z = t; }
@@ -59,6 +59,11 @@ __device__ __forceinline__ bool box_hit(vec3f o, vec3f invd, float tmin_r, float
     tmax *= 1.00000024f;
     tnear = tmin;
     return tmin <= tmax;
+}
+
+__device__ __forceinline__ bool box_hit(vec3f o, vec3f invd, float tmin_r, float tmax_r, float4 lo, float4 hi,
+                                        float& tnear) {
+    return box_hit6(o, invd, tmin_r, tmax_r, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, tnear);
 }
 
 __device__ __forceinline__ bool box_hit(vec3f o, vec3f invd, float tmin_r, float tmax_r, float4 lo, float4 hi) {

@@ -141,7 +141,12 @@ struct tracer {
     SE* lane_stk;
     __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
                                           work_counts& wc) {
-        if (PACKET) return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
+        if (PACKET) {
+#ifndef YRT_NO_WIDE
+            if (ANY && !COUNT && S.wide) return packet_occluded_wide(S, ray, valid);
+#endif
+            return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
+        }
         if (!valid) return false;
         if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
         return traverse<false, COUNT, WF_BLOCK>(S, ray, hr, lane_stk, wc);

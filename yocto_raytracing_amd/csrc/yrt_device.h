@@ -4,8 +4,9 @@
 // Everything is 16-byte records so each fetch is one global_load_dwordx4:
 //   tnodes  2 x f4 per instance-BVH node  {min.xyz, start} {max.xyz, count|leaf<<31}
 //   tinst   4 x f4 per instance-BVH leaf slot (instances permuted to leaf order)
-//           {frame.x, shape} {frame.y, instance id} {frame.z, material}
+//           {frame.x, shape} {frame.y, shape wide root | kind << 30} {frame.z, material}
 //           {frame.o, shape root node | kind << 30}
+//   tinst_id int per instance-BVH leaf slot: the instance's index in the scene
 //   snodes  2 x f4 per shape-BVH node, all shapes concatenated, child/leaf indices absolute
 //   sprims  3 x f4 per shape-BVH leaf slot (primitives permuted to leaf order)
 //           triangle {v0, ei} {v1-v0, -} {v2-v0, -}   (the reference's e1/e2, scene.cpp:232-233)
@@ -18,6 +19,9 @@
 //   lights  6 x f4 {frame.x} {frame.y} {frame.z} {frame.o} {pos0 of the light shape} {ke}
 //   texels  RGBA8 of every texture; texinfo i4 {offset, width, height, -}
 //   srgb    256 floats: fmin(1, pow(c/255, 2.2)) (raytrace.cpp:51-53) precomputed on the host
+//   wnodes  8 x f4 per 4-wide node of the any-hit walk (device_scene.cpp wide_builder):
+//           {lo.x[4]} {lo.y[4]} {lo.z[4]} {hi.x[4]} {hi.y[4]} {hi.z[4]} {ref[4]} {info[4]},
+//           instance level and all shapes in one array, absolute indices
 #pragma once
 
 #include <stdint.h>
@@ -54,6 +58,10 @@ struct dev_scene_view {
     const uint32_t* texels;
     const i4* texinfo;
     const float* srgb;
+    const f4* wnodes;
+    const int* tinst_id;
+    int wtop_root;
+    int wide;  // 1: any-hit queries use the 4-wide walk
     int nlights;
     int ntnodes;
 };

@@ -54,6 +54,7 @@ struct device_scene {
     size_t max_shape_nodes = 0;
     bool narrow_stack = true;  // all node indices fit 16-bit stack entries
     bool reflective = false;   // any material with kr > 0 (bounce levels needed)
+    bool wide_ok = false;      // the 4-wide any-hit walk's stack fits (else the binary walk)
     int nlights = 0;
     // wavefront workspace (device), grown on demand
     void* work = nullptr;
@@ -74,7 +75,7 @@ hipError_t launch_render(device_scene& ds, const dev_render_args& args, void* ou
                          unsigned long long* counters, bool count_work, hipStream_t stream);
 hipError_t launch_trace(const device_scene& ds, const float* rays, int n, int any,
                         unsigned char* hit, int* inst, int* ei, float* ew, float* dist,
-                        unsigned long long* counters, hipStream_t stream);
+                        unsigned long long* counters, bool packet, hipStream_t stream);
 hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, hipStream_t stream);
 
 // traversal stack entries per lane (LDS resident): instance level + shape level
