@@ -161,13 +161,18 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
     const vec3f wo = wray.o, wd = wray.d;
-    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
     const float tmin = wray.tmin;
     float tmax = wray.tmax;
-    vec3f co = wo, cd = wd, ci = wi;  // ray of the current level (local inside an instance)
+    // ray of the current level (local inside an instance); the world inverse direction
+    // is recomputed when the walk leaves an instance leaf rather than kept live
+    vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
     // per-lane flags are kept as ints (VGPRs): a bool carried around the loop becomes
     // a 64-bit lane mask merged with exec on every back edge (scalar work per step)
     int hit = 0;
+    // closest hit so far: barycentrics w1, w2 only (ew = {1-w1-w2, w1, w2, 0} for every
+    // primitive kind, rebuilt at the end with the reference's arithmetic); its distance
+    // is tmax
+    float hw1 = 0, hw2 = 0;
     // the stack: slot s of each of these VGPRs is lane s
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0;       // lanes out of the walk (any-hit found / NaN tmax)
@@ -240,25 +245,26 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     const float4 a = pv[0], b = pv[1], c = pv[2];
                     if (COUNT && in && !(ANY && leaf_hit)) wc.prim++;
                     if (COUNT && lane == 0) wc.wprim++;
-                    float t;
-                    vec4f ew;
+                    float t, w1, w2;
                     bool h;
                     if (kind == kind_triangles) {
-                        float w1, w2;
                         h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2);
-                        ew = {1 - w1 - w2, w1, w2, 0};
                     } else {
+                        // lines: ew = {1-s, s, 0, 0}; points: {1, 0, 0, 0} -- both are
+                        // {1-w1-w2, w1, w2, 0} with w1 = ew.y, w2 = ew.z
+                        vec4f ew;
                         const ray3 lr = {co, cd, tmin, tmax};
                         h = kind == kind_lines ? line_hit(lr, xyz(a), xyz(b), b.w, c.x, t, ew)
                                                : point_hit(lr, xyz(a), b.x, t, ew);
+                        w1 = ew.y, w2 = ew.z;
                     }
                     h = h && in;
                     if (!ANY) {
                         tmax = h ? t : tmax;
                         hr.slot = h ? cur_slot : hr.slot;
                         hr.ei = h ? ibits(a.w) : hr.ei;
-                        hr.ew = h ? ew : hr.ew;
-                        hr.dist = h ? t : hr.dist;
+                        hw1 = h ? w1 : hw1;
+                        hw2 = h ? w2 : hw2;
                     }
                     leaf_hit |= h ? 1 : 0;
                 }
@@ -297,9 +303,15 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                 nbase = S.tnodes;
                 co = wo;
                 cd = wd;
-                ci = wi;
+                ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
             }
-            if (sp == 0) return hit;
+            if (sp == 0) {
+                if (!ANY && hit) {
+                    hr.ew = {1 - hw1 - hw2, hw1, hw2, 0};
+                    hr.dist = tmax;
+                }
+                return hit;
+            }
             sp--;
             node = __builtin_amdgcn_readlane(stk_node, sp);
             const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp);

@@ -141,12 +141,7 @@ struct tracer {
     SE* lane_stk;
     __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
                                           work_counts& wc) {
-        if (PACKET) {
-#ifndef YRT_NO_WIDE
-            if (ANY && !COUNT && S.wide) return packet_occluded_wide(S, ray, valid);
-#endif
-            return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
-        }
+        if (PACKET) return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
         if (!valid) return false;
         if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
         return traverse<false, COUNT, WF_BLOCK>(S, ray, hr, lane_stk, wc);
@@ -249,7 +244,9 @@ __global__ __launch_bounds__(WF_BLOCK) void k_bounce(dev_scene_view S, int level
 }
 
 // ---- shadow rays (raytrace.cpp:128-133): one light per blockIdx.y ----
-template <bool COUNT, bool PACKET, typename SE>
+// WIDE: the 4-wide any-hit walk (timed kernels on scenes whose wide stack fits);
+// otherwise the tracer's binary walk (and always for the instrumented COUNT pass)
+template <bool COUNT, bool PACKET, typename SE, bool WIDE>
 __global__ __launch_bounds__(WF_BLOCK) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
                                                      unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
@@ -280,7 +277,11 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shadow(dev_scene_view S, int level
             }
         }
         hit_record hr;
-        const bool occ = T.trace(S, sr, valid, hr, wc);
+        bool occ;
+        if constexpr (WIDE)
+            occ = packet_occluded_wide(S, sr, valid);
+        else
+            occ = T.trace(S, sr, valid, hr, wc);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
     }
     // shadow rays are counted once, here; yrt_last_stats reports rays = cnt_rays + this
@@ -538,8 +539,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid : grid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
-                hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE>), sg, dim3(WF_BLOCK), YRT_EXP_SHADOW_LDS, stream, ds.view, level, nsamp, B,
-                                   counters);
+                if (!COUNT && PACKET && ds.wide_ok)
+                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(WF_BLOCK), YRT_EXP_SHADOW_LDS,
+                                       stream, ds.view, level, nsamp, B, counters);
+                else
+                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, false>), sg, dim3(WF_BLOCK), YRT_EXP_SHADOW_LDS,
+                                       stream, ds.view, level, nsamp, B, counters);
                 T.end(t, stream);
             }
             t = T.begin(phase_shade, stream);
