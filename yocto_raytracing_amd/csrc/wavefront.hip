@@ -35,6 +35,9 @@ namespace yrt {
 namespace {
 
 constexpr int WF_BLOCK = 256;
+#ifndef YRT_TRACE_WAVES
+#define YRT_TRACE_WAVES 7  // waves per SIMD the traversal kernels are register-budgeted for (A/B: 6 -> 7 is -5 %, 8 spills too much)
+#endif
 #ifndef YRT_EXP_SHADOW_LDS
 #define YRT_EXP_SHADOW_LDS 0  // experiment knob: dynamic LDS per shadow block (occupancy cap)
 #endif
@@ -173,7 +176,7 @@ __device__ __forceinline__ tracer<ANY, COUNT, PACKET, SE> make_tracer(traversal_
 
 // ---- level 0: camera rays + closest hit + surface ----
 template <bool COUNT, bool PACKET, typename SE>
-__global__ __launch_bounds__(WF_BLOCK) void k_primary(dev_scene_view S, dev_render_args A, chunk_args C,
+__global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A, chunk_args C,
                                                       wf_buffers B, unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_primary(dev_scene_view S, dev_rend
 
 // ---- levels >= 1: closest hit of the compacted mirror rays (grid-stride) ----
 template <bool COUNT, bool PACKET, typename SE>
-__global__ __launch_bounds__(WF_BLOCK) void k_bounce(dev_scene_view S, int level, wf_buffers B,
+__global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_view S, int level, wf_buffers B,
                                                      unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_bounce(dev_scene_view S, int level
 // WIDE: the 4-wide any-hit walk (timed kernels on scenes whose wide stack fits);
 // otherwise the tracer's binary walk (and always for the instrumented COUNT pass)
 template <bool COUNT, bool PACKET, typename SE, bool WIDE>
-__global__ __launch_bounds__(WF_BLOCK) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
+__global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
                                                      unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
