@@ -352,8 +352,23 @@ __device__ __forceinline__ bool occluded(const dev_scene_view& S, const ray3& wr
     }
 }
 
-// specular exponent: the reference calls powf; evaluate in f64 and round once
-__device__ __forceinline__ float powf_cr(float x, float y) { return (float)pow((double)x, (double)y); }
+// specular exponent: the reference calls powf; evaluate in f64 and round once.
+// Bases here are >= 0 (max(0, n.h) or sqrt(1-|n.h|)) or NaN. exp2(y*log2(x)) in f64
+// carries a relative error of about |y*log2 x| * 2^-52 (< 2^-44 until the result
+// underflows f32), so the single rounding to f32 is the correctly rounded powf except
+// within ~2^-20 ulp of a rounding boundary -- the same exposure as a full f64 pow at a
+// fraction of its cost. pow(x, 0) = 1 for every x (log2(0) * 0 would be NaN).
+#ifndef YRT_POW_FULL
+#define YRT_POW_FULL 0
+#endif
+__device__ __forceinline__ float powf_cr(float x, float y) {
+#if YRT_POW_FULL
+    return (float)pow((double)x, (double)y);
+#else
+    if (y == 0.0f) return 1.0f;
+    return (float)exp2((double)y * log2((double)x));
+#endif
+}
 
 // lookup_texture + eval_texture (raytrace.cpp:39-86), srgb always on. fmod(u,1)*w in
 // double equals the f32 product: the fmod is exact and the product of two floats is
