@@ -299,10 +299,15 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_shadow(dev_scene_
 }
 
 // ---- shade() after the queries (raytrace.cpp:99-206) ----
-template <bool COUNT>
+// FUSE (level 0 of a scene without mirrors, s*s dividing the block): the block's
+// samples are whole pixels, so the ordered per-pixel sum of k_accumulate is done here
+// from LDS and the per-sample radiance never goes to HBM.
+template <bool COUNT, bool FUSE>
 __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
-                                                    int max_depth, wf_buffers B, unsigned long long* counters) {
+                                                    int max_depth, wf_buffers B, unsigned long long* counters,
+                                                    chunk_args C, float4* __restrict__ out) {
     const int n = level ? B.count[level] : nsamp_level0;
+    __shared__ float4 fused_rad[FUSE ? WF_BLOCK : 1];
     work_counts wc;
     unsigned long long truncated = 0;
     const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
@@ -388,7 +393,9 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                 }
                 if (COUNT) wc.hits++;
             }
-            if (write_r) {
+            if (FUSE) {
+                fused_rad[threadIdx.x] = make_float4(R.x, R.y, R.z, 1.0f);
+            } else if (write_r) {
                 f4* dst = level ? B.R[level] : B.rad;
                 dst[idx] = {R.x, R.y, R.z, 1.0f};
             }
@@ -409,6 +416,30 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                 B.rec0[level][idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
                 B.rec1[level][idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
                 B.rec2[level][idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
+            }
+        }
+    }
+    if (FUSE) {
+        // raytrace.cpp:232-249: s*s samples of a pixel summed in jj/ii order, then / s*s
+        __syncthreads();
+        const int ppb = WF_BLOCK / C.spp;
+        if ((int)threadIdx.x < ppb) {
+            const int pl = (int)(blockIdx.x * WF_BLOCK / C.spp) + threadIdx.x;
+            int lx, ly, i, j;
+            const bool valid = pl < C.npix && pixel_of(A, C.tiles_x, C.pix0 + pl, lx, ly, i, j);
+            if (pl < C.npix && lx < A.tile_w && ly < A.tile_h) {
+                float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (valid) {
+                    vec4f acc = {0, 0, 0, 0};
+                    const float4* r = fused_rad + threadIdx.x * C.spp;
+                    for (int q = 0; q < C.spp; q++) {
+                        const float4 c = r[q];
+                        acc = {acc.x + c.x, acc.y + c.y, acc.z + c.z, acc.w + 1.0f};
+                    }
+                    const float d = float(C.spp);
+                    o = make_float4(acc.x / d, acc.y / d, acc.z / d, 1.0f);
+                }
+                out[(size_t)ly * A.out_stride + lx] = o;
             }
         }
     }
@@ -521,6 +552,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
     phase_timer& T = ds.timer;
     const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
+    // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE)
+#ifndef YRT_NO_FUSE
+    const bool fuse = nlevels == 1 && WF_BLOCK % spp == 0;
+#else
+    const bool fuse = false;
+#endif
     for (long long pix0 = 0; pix0 < npix_total; pix0 += pix_per_chunk) {
         chunk_args C = {pix0, (int)std::min<long long>(pix_per_chunk, npix_total - pix0), spp, tiles_x};
         const int nsamp = C.npix * spp;
@@ -551,8 +588,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 T.end(t, stream);
             }
             t = T.begin(phase_shade, stream);
-            hipLaunchKernelGGL((k_shade<COUNT>), dim3(level ? stride_grid : grid), dim3(WF_BLOCK), 0, stream, ds.view,
-                               A, level, nsamp, A.max_depth, B, counters);
+            if (fuse)
+                hipLaunchKernelGGL((k_shade<COUNT, true>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, level,
+                                   nsamp, A.max_depth, B, counters, C, out);
+            else
+                hipLaunchKernelGGL((k_shade<COUNT, false>), dim3(level ? stride_grid : grid), dim3(WF_BLOCK), 0,
+                                   stream, ds.view, A, level, nsamp, A.max_depth, B, counters, C, out);
             T.end(t, stream);
         }
         for (int level = nlevels - 2; level >= 0; level--) {
@@ -560,10 +601,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             hipLaunchKernelGGL(k_fold_children, dim3(stride_grid), dim3(WF_BLOCK), 0, stream, level, B);
             T.end(t, stream);
         }
-        t = T.begin(phase_accumulate, stream);
-        hipLaunchKernelGGL(k_accumulate, dim3((C.npix + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream, A, C,
-                           B, out);
-        T.end(t, stream);
+        if (!fuse) {
+            t = T.begin(phase_accumulate, stream);
+            hipLaunchKernelGGL(k_accumulate, dim3((C.npix + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream, A,
+                               C, B, out);
+            T.end(t, stream);
+        }
     }
     return hipGetLastError();
 }
