@@ -96,9 +96,18 @@ __device__ __forceinline__ float4 rec_of(const V& v, int k) {
     return {__int_as_float(v[4 * k]), __int_as_float(v[4 * k + 1]), __int_as_float(v[4 * k + 2]),
             __int_as_float(v[4 * k + 3])};
 }
+// the address as SGPRs (a no-op when the compiler already holds it there; where its
+// uniformity analysis lost track, one v_readfirstlane per half)
+__device__ __forceinline__ const f4* sgpr_ptr(const f4* p) {
+    const unsigned long long a = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    return (const f4*)((unsigned long long)hi << 32 | lo);
+}
+
 template <int N>
-__device__ __forceinline__ void ld_scalar(const f4* p, float4 (&out)[N]) {
+__device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
     static_assert(N == 2 || N == 3 || N == 4 || N == 8, "record count");
+    const f4* p = sgpr_ptr(p_);
     if constexpr (N == 2) {
         sgpr8 a;
         asm volatile("s_load_dwordx8 %0, %1, 0x0\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
@@ -360,7 +369,8 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 float tn;
-                m[k] = ballot(in[k] != 0 && box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)) &
+                m[k] = ballot(in[k] != 0 &&
+                              box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)) &
                        mask;
             }
             int first = -1;
