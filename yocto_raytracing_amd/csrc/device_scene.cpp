@@ -263,6 +263,37 @@ device_scene* device_scene_create(const scene& scn, int device) {
         tnodes.push_back(node_lo(n, n.start));
         tnodes.push_back(node_hi(n));
     }
+    // pair records for the closest-hit walk: node X's record followed by the record of
+    // X's child start+1 (the node the reference tests right after X), 64 bytes
+    auto pairs = [](const std::vector<f4>& nodes, size_t first, size_t count, size_t base) {
+        std::vector<f4> out;
+        out.reserve(count * 4);
+        for (size_t x = first; x < first + count; x++) {
+            const f4 lo = nodes[2 * x], hi = nodes[2 * x + 1];
+            out.push_back(lo);
+            out.push_back(hi);
+            uint32_t cl;
+            memcpy(&cl, &hi.w, 4);
+            if (cl & leaf_bit) {
+                out.push_back({0, 0, 0, 0});
+                out.push_back({0, 0, 0, 0});
+            } else {
+                uint32_t start;
+                memcpy(&start, &lo.w, 4);
+                const size_t c1 = base + start + 1;
+                out.push_back(nodes[2 * c1]);
+                out.push_back(nodes[2 * c1 + 1]);
+            }
+        }
+        return out;
+    };
+    std::vector<f4> tpair = pairs(tnodes, 0, tnodes.size() / 2, 0);
+    std::vector<f4> spair;
+    for (size_t si = 0; si < scn.shapes.size(); si++) {
+        const size_t nb = (size_t)shapes[si].x, nn = scn.shapes[si].bvh.nodes.size();
+        std::vector<f4> p = pairs(snodes, nb, nn, nb);
+        spair.insert(spair.end(), p.begin(), p.end());
+    }
     for (int ii : scn.bvh.leaf_prims) {
         const instance& ist = scn.instances[ii];
         if (ist.mat < 0 || ist.mat >= (int)scn.materials.size())
@@ -342,6 +373,8 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_texinfo = ab.add(texinfo.data(), texinfo.size() * sizeof(i4));
     size_t o_srgb = ab.add(srgb.data(), srgb.size() * sizeof(float));
     size_t o_wnodes = ab.add(wnodes.data(), wnodes.size() * sizeof(f4));
+    size_t o_tpair = ab.add(tpair.data(), tpair.size() * sizeof(f4));
+    size_t o_spair = ab.add(spair.data(), spair.size() * sizeof(f4));
     size_t o_tinst_id = ab.add(tinst_id.data(), tinst_id.size() * sizeof(int));
 
     try {
@@ -373,6 +406,8 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.texinfo = (const i4*)(base + o_texinfo);
     v.srgb = (const float*)(base + o_srgb);
     v.wnodes = (const f4*)(base + o_wnodes);
+    v.tpair = (const f4*)(base + o_tpair);
+    v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);
     v.wtop_root = wtop_root;
     v.wide = ds->wide_ok ? 1 : 0;

@@ -44,6 +44,13 @@
 namespace yrt {
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// this lane's index, computed where it is used (two v_mbcnt) instead of being held in
+// a VGPR across the walk -- under register pressure the compiler otherwise spills it
+__device__ __forceinline__ int lane_now() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n v_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ float lane_value(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -188,64 +195,77 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
     unsigned long long inst_mask = 0;  // lanes entering the current instance leaf
     int level = 0, sp = 0, base = 0, root = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
     int node = 0;
-    const f4* nbase = S.tnodes;  // node array of the current level (the shape's nodes at level 1)
+    // pair records of the current level (yrt_device.h tpair/spair): node X's record and
+    // that of its child start+1, so one fetch serves the two tests the reference makes
+    // back to back (test X; push start; pop start+1 and test it -- no primitive test
+    // and so no tmax change in between)
+    const f4* pbase = S.tpair;
     unsigned long long mask = live;
     for (;;) {
         // ---- every lane of `mask` tests `node` with its own ray ----
-        const f4* nb = nbase + 2 * node;
-        float4 rec[2];
-        ld_records<2>(nb, rec);
+        node = uniform(node);  // keep the node index (and the address math) scalar
+        float4 rec[4];
+        ld_records<4>(pbase + 4 * node, rec);
         const float4 lo = rec[0], hi = rec[1];
         if (COUNT && (mask & me)) wc.box++;
         if (COUNT && lane == 0) wc.wnode++;
         const unsigned long long pm = ballot(box_hit(co, ci, tmin, tmax, lo, hi)) & mask;
-#ifdef YRT_EXP_VALU2  // diagnostic: a second, unused box test per step
-        {
-            bool b2 = box_hit(co, ci, tmin * 0.5f, tmax * 0.5f, lo, hi);
-            asm volatile("" ::"v"((int)b2));
-        }
-#endif
-#ifdef YRT_EXP_SALU  // diagnostic: 16 dependent scalar adds per step
-        {
-            int d = node;
-            asm volatile(
-                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
-                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
-                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
-                "s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n s_add_u32 %0, %0, 1\n"
-                : "+s"(d));
-        }
-#endif
+        // the child start+1, tested now with the same tmax (used only if X is inner and passes)
+        const bool pass1 = box_hit(co, ci, tmin, tmax, rec[2], rec[3]);
 #ifdef YRT_EXP_LAT  // diagnostic: one more dependent fetch per step
         {
-            float4 again = ld4_whole(nbase + 2 * (node ^ (int)(pm & 1)));
-            asm volatile("" ::"v"(again.x));
+            float4 again[2];
+            ld_records<2>(pbase + 4 * (node ^ (int)(pm & 1)), again);
+            asm volatile("" ::"v"(again[0].x));
         }
 #endif
+        // the leaf to process after this step, if any: first slot, count|leaf, lanes
+        int lstart = 0;
+        uint32_t lcl = 0;
+        unsigned long long lmask = 0;
         if (pm) {
             const int start = uniform(ibits(lo.w));
             const uint32_t cl = (uint32_t)uniform((int)ubits(hi.w));
             if (!(cl & leaf_bit)) {
-                // push start, continue with start+1 (the reference pops start+1 first)
-                // slot sp of the stack VGPRs := {start, pm} (one compare + three selects)
-                const bool at = lane == sp;
+                // push start (slot sp of the stack VGPRs := {start, pm}); the reference
+                // pops start+1 next and tests it: that is pass1
+                bool at = lane_now() == sp;
                 stk_node = at ? start : stk_node;
                 stk_mlo = at ? (int)(uint32_t)pm : stk_mlo;
                 stk_mhi = at ? (int)(uint32_t)(pm >> 32) : stk_mhi;
                 sp++;
-                node = start + 1;
-                mask = pm;
-                continue;
+                if (COUNT && (pm & me)) wc.box++;
+                const unsigned long long p1 = ballot(pass1) & pm;
+                if (p1) {
+                    const int start1 = uniform(ibits(rec[2].w));
+                    const uint32_t cl1 = (uint32_t)uniform((int)ubits(rec[3].w));
+                    if (!(cl1 & leaf_bit)) {
+                        at = lane_now() == sp;
+                        stk_node = at ? start1 : stk_node;
+                        stk_mlo = at ? (int)(uint32_t)p1 : stk_mlo;
+                        stk_mhi = at ? (int)(uint32_t)(p1 >> 32) : stk_mhi;
+                        sp++;
+                        node = start1 + 1;
+                        mask = p1;
+                        continue;
+                    }
+                    lstart = start1, lcl = cl1, lmask = p1;
+                }
+            } else {
+                lstart = start, lcl = cl, lmask = pm;
             }
-            const int count = (int)(cl & 0xffffu);
+        }
+        if (lmask) {
+            const int start = lstart;
+            const int count = (int)(lcl & 0xffffu);
             if (level == 0) {
                 inst_next = start;
                 inst_end = start + count;
-                inst_mask = pm;
+                inst_mask = lmask;
                 level = 1;
                 base = sp;
             } else {
-                const bool in = (pm >> lane) & 1;
+                const bool in = (lmask >> lane) & 1;
                 int leaf_hit = 0;
                 for (int i = start; i < start + count; i++) {
                     const f4* pr = S.sprims + 3 * i;
@@ -300,7 +320,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     const uint32_t rk = (uint32_t)uniform(ibits(fo.w));
                     root = (int)(rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
-                    nbase = S.snodes + 2 * root;
+                    pbase = S.spair + 4 * root;
                     cur_slot = k;
                     node = 0;  // the shape root, tested like any popped node
                     mask = inst_mask & ~done;
@@ -309,7 +329,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     continue;
                 }
                 level = 0;
-                nbase = S.tnodes;
+                pbase = S.tpair;
                 co = wo;
                 cd = wd;
                 ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
@@ -381,7 +401,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
                     first = k;
                     continue;
                 }
-                const bool at = lane == sp;
+                const bool at = lane_now() == sp;
                 stk_ref = at ? rf[k] : stk_ref;
                 stk_info = at ? in[k] : stk_info;
                 stk_mlo = at ? (int)(uint32_t)m[k] : stk_mlo;

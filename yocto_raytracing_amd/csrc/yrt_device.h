@@ -59,6 +59,8 @@ struct dev_scene_view {
     const i4* texinfo;
     const float* srgb;
     const f4* wnodes;
+    const f4* tpair;  // 4 x f4 per instance-BVH node: its record + its child start+1's
+    const f4* spair;  // the same for the shape BVHs (same indexing as snodes)
     const int* tinst_id;
     int wtop_root;
     int wide;  // 1: any-hit queries use the 4-wide walk
