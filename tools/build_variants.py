@@ -21,23 +21,23 @@ def main(argv):
     b.build_library()
     out_dir = PKG / "variants"
     out_dir.mkdir(exist_ok=True)
-    host_objs = [b.BUILD / (Path(s).stem + ".o") for s in b.SOURCES if not s.endswith(".hip")]
     for spec in argv:
         name, _, defs = spec.partition(":")
         defines = [d for d in defs.split(",") if d]
         vdir = out_dir / name
         vdir.mkdir(exist_ok=True)
         objs = []
-        for src in b.SOURCES:
-            if not src.endswith(".hip"):
-                continue
+        for src in b.SOURCES:  # host and device code both see the defines
             o = vdir / (Path(src).stem + ".o")
-            subprocess.run([b.HIPCC, *b.COMMON, *defines, f"--offload-arch={b.ARCH}", "-c", str(b.CSRC / src),
-                            "-o", str(o)], check=True, capture_output=True)
+            if src.endswith(".hip"):
+                cmd = [b.HIPCC, *b.COMMON, *defines, f"--offload-arch={b.ARCH}", "-c", str(b.CSRC / src), "-o", str(o)]
+            else:
+                cmd = [b.CLANGXX, *b.COMMON, *b.HOST_DEFS, *defines, "-c", str(b.CSRC / src), "-o", str(o)]
+            subprocess.run(cmd, check=True, capture_output=True)
             objs.append(o)
         lib = out_dir / f"libyrt_{name}.so"
-        subprocess.run([b.HIPCC, "-shared", "-fPIC", f"--offload-arch={b.ARCH}", "-o", str(lib),
-                        *map(str, host_objs + objs), "-lz"], check=True)
+        subprocess.run([b.HIPCC, "-shared", "-fPIC", f"--offload-arch={b.ARCH}", "-o", str(lib), *map(str, objs), "-lz"],
+                       check=True)
         print(lib)
 
 

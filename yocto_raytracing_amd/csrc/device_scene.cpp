@@ -13,6 +13,7 @@
 //     the same calls the reference makes per shading point
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -89,6 +90,25 @@ struct wide_builder {
                 }
             }
         }
+        // The any-hit walk enters the first passing slot and pops the others in slot
+        // order; the order does not change any answer. Smallest surface area first
+        // (A/B at c4: shadow -2.7 %; largest first +1.7 %).
+#ifndef YRT_WIDE_SORT
+#define YRT_WIDE_SORT -1
+#endif
+        auto area = [&](int i) {
+            const bbox3f& b = t.nodes[i].bbox;
+            const vec3f d = b.max - b.min;
+            return d.x * d.y + d.y * d.z + d.z * d.x;
+        };
+        if (YRT_WIDE_SORT == 2)  // leaves first, then smallest
+            std::stable_sort(slots.begin(), slots.end(), [&](int a, int b) {
+                const bool la = t.nodes[a].isleaf, lb = t.nodes[b].isleaf;
+                return la != lb ? la : area(a) < area(b);
+            });
+        else if (YRT_WIDE_SORT != 0)
+            std::stable_sort(slots.begin(), slots.end(),
+                             [&](int a, int b) { return YRT_WIDE_SORT > 0 ? area(a) > area(b) : area(a) < area(b); });
         const int me = (int)out.size() / 8;
         out.resize(out.size() + 8, f4{0, 0, 0, 0});
         float v[6][4];
