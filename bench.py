@@ -181,6 +181,8 @@ def main():
     kernel_names = {"megakernel": "render_kernel<false>"}
     for ph in ("primary", "shadow", "bounce"):
         kernel_names[ph] = f"k_{ph}{targs.get(a.algorithm, '')}"
+    if a.algorithm == "wavefront":  # the timed shadow kernel walks the 4-wide collapse
+        kernel_names["shadow"] = "k_shadow<false, true, unsigned int, true>"
 
     def step(timing=0):
         params.timing = timing
