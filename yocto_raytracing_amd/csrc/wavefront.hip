@@ -308,6 +308,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                                                     chunk_args C, float4* __restrict__ out) {
     const int n = level ? B.count[level] : nsamp_level0;
     __shared__ float4 fused_rad[FUSE ? WF_BLOCK : 1];
+    __shared__ int cmp_count[WF_BLOCK / 64], cmp_base[WF_BLOCK / 64];
     work_counts wc;
     unsigned long long truncated = 0;
     const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
@@ -400,23 +401,29 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                 dst[idx] = {R.x, R.y, R.z, 1.0f};
             }
         }
-        // wave compaction of the mirror rays: one atomic per wave, lanes take
-        // consecutive slots in lane order
+        // compaction of the mirror rays: one atomic per BLOCK (a shared counter hit by
+        // every wave serialises); waves take consecutive ranges in wave order, lanes
+        // consecutive slots in lane order (the fold follows parent indices, so the
+        // order is free)
+        if constexpr (FUSE) continue;  // one level: no mirror rays
         const unsigned long long mask = __ballot(spawn);
-        if (mask) {
-            int base = 0;
-            const int lane = threadIdx.x & 63;
-            const int first = __ffsll((long long)mask) - 1;
-            if (lane == first) base = atomicAdd(B.count + level + 1, __popcll(mask));
-            base = __shfl(base, first, 64);
-            if (spawn) {
-                const int slot = base + __popcll(mask & ((1ull << lane) - 1));
-                B.ray_o[level + 1][slot] = {p.x, p.y, p.z, __int_as_float(idx)};
-                B.ray_d[level + 1][slot] = {dr.x, dr.y, dr.z, 0};
-                B.rec0[level][idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
-                B.rec1[level][idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
-                B.rec2[level][idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
-            }
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (lane == 0) cmp_count[w] = __popcll(mask);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int q = 0; q < WF_BLOCK / 64; q++) tot += cmp_count[q];
+            int acc = tot ? atomicAdd(B.count + level + 1, tot) : 0;
+            for (int q = 0; q < WF_BLOCK / 64; q++) cmp_base[q] = acc, acc += cmp_count[q];
+        }
+        __syncthreads();
+        if (spawn) {
+            const int slot = cmp_base[w] + __popcll(mask & ((1ull << lane) - 1));
+            B.ray_o[level + 1][slot] = {p.x, p.y, p.z, __int_as_float(idx)};
+            B.ray_d[level + 1][slot] = {dr.x, dr.y, dr.z, 0};
+            B.rec0[level][idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
+            B.rec1[level][idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
+            B.rec2[level][idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
         }
     }
     if (FUSE) {
