@@ -128,13 +128,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on fewer GPUs (e.g. 2 ranks on one card with gloo):
+    # YRT_BENCH_DEVICES=1 maps rank r to device r % 1; the driver's runs never set it
+    ndev_override = int(os.environ.get("YRT_BENCH_DEVICES", "0"))
+    if ndev_override > 0:
+        local = local % ndev_override
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N>1 needs one process per GPU: launch with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("YRT_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import yocto_raytracing_amd as yrt
 
