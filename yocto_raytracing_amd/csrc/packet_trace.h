@@ -352,6 +352,13 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
 }
 
 
+#ifndef YRT_WIDE_HOIST
+#define YRT_WIDE_HOIST 0  // 1: slab-swap signs hoisted to level changes (A/B: +2 %)
+#endif
+#ifndef YRT_WIDE_SKIP
+#define YRT_WIDE_SKIP 1  // scalar branch around empty slots (A/B: shadow -3 %)
+#endif
+
 // ---- any-hit on the 4-wide collapse (device_scene.cpp wide_builder) ----
 // The same packet discipline (SGPR control, VGPR-lane stack, lane masks), over wide
 // nodes: a visit fetches one 128-byte record and every lane of the mask tests the
@@ -361,6 +368,18 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
 // walk at its first hit. Results equal intersect_any's (see wide_builder for why the
 // skipped inner boxes and the order do not matter); the instrumented (COUNT) kernels
 // use the binary walk instead, so work counts stay the reference's.
+#ifdef YRT_WIDE_STATS  // diagnostic: wave-level step counts of the wide walk
+__device__ unsigned long long g_wide_stats[8];
+#define WSTAT(k) \
+    do {                                                                \
+        if (__lane_id() == 0) atomicAdd(&g_wide_stats[(k)], 1ull); \
+    } while (0)
+#else
+#define WSTAT(k) \
+    do {           \
+    } while (0)
+#endif
+
 __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, const ray3& wray, bool valid) {
     const int lane = __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
@@ -369,6 +388,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
     const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
     const float tmin = wray.tmin, tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = wi;
+    bool sx = ci.x < 0, sy = ci.y < 0, sz = ci.z < 0;  // slab swaps, per ray and level
     int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
@@ -378,6 +398,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
     unsigned long long mask = live;
     for (;;) {
         if (!(info & leaf_bit)) {
+            WSTAT(0);
             float4 r[8];
             ld_records<8>(S.wnodes + 8 * ref, r);
             const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
@@ -388,10 +409,20 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
             unsigned long long m[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
+#if YRT_WIDE_HOIST
+#define WIDE_BOX(k) box_hit6s(co, ci, sx, sy, sz, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])
+#else
+#define WIDE_BOX(k) box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)
+#endif
                 float tn;
-                m[k] = ballot(in[k] != 0 &&
-                              box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)) &
-                       mask;
+#if YRT_WIDE_SKIP
+                m[k] = 0;
+                // empty slots (info 0) are skipped on a scalar branch
+                if (uniform(in[k]) != 0) m[k] = ballot(WIDE_BOX(k)) & mask;
+#else
+                m[k] = ballot(in[k] != 0 && WIDE_BOX(k)) & mask;
+#endif
+#undef WIDE_BOX
             }
             int first = -1;
 #pragma unroll
@@ -417,12 +448,14 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
                 continue;
             }
         } else if (level == 0) {
+            WSTAT(1);
             inst_next = ref;
             inst_end = ref + (int)(info & 0xffffu);
             inst_mask = mask;
             level = 1;
             base = sp;
         } else {
+            WSTAT(2);
             const bool inl = (mask >> lane) & 1;
             int leaf_hit = 0;
             const int count = (int)(info & 0xffffu);
@@ -449,6 +482,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
         for (;;) {
             if (level == 1 && sp == base) {
                 if (inst_next < inst_end) {
+                    WSTAT(3);
                     const int k = inst_next++;
                     float4 fr[4];
                     ld_records<4>(S.tinst + 4 * k, fr);
@@ -456,6 +490,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
                     co = transform_point_inverse(f, wo);
                     cd = transform_direction_inverse(f, wd);
                     ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    sx = ci.x < 0, sy = ci.y < 0, sz = ci.z < 0;
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
                     ref = (int)(rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
@@ -468,8 +503,10 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
                 co = wo;
                 cd = wd;
                 ci = wi;
+                sx = ci.x < 0, sy = ci.y < 0, sz = ci.z < 0;
             }
             if (sp == 0) return (done >> lane) & 1;
+            WSTAT(4);
             sp--;
             ref = __builtin_amdgcn_readlane(stk_ref, sp);
             info = (uint32_t)__builtin_amdgcn_readlane(stk_info, sp);

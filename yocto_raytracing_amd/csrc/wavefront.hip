@@ -637,3 +637,15 @@ hipError_t launch_render_wavefront(device_scene& ds, const dev_render_args& args
 }
 
 }  // namespace yrt
+
+#ifdef YRT_WIDE_STATS
+extern "C" int yrt_debug_wide_stats(unsigned long long* out8, int reset) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(yrt::g_wide_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_wide_stats), z, sizeof z);
+    }
+    return 0;
+}
+#endif
