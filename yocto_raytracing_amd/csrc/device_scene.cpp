@@ -283,26 +283,31 @@ device_scene* device_scene_create(const scene& scn, int device) {
         tnodes.push_back(node_lo(n, n.start));
         tnodes.push_back(node_hi(n));
     }
-    // pair records for the closest-hit walk: node X's record followed by the record of
-    // X's child start+1 (the node the reference tests right after X), 64 bytes
+    // spine records for the closest-hit walk: node X's record followed by those of its
+    // child start+1, that child's child start+1, ... (spine_len nodes, 32 bytes each):
+    // the nodes the reference tests back to back after X when each one passes
     auto pairs = [](const std::vector<f4>& nodes, size_t first, size_t count, size_t base) {
         std::vector<f4> out;
-        out.reserve(count * 4);
+        out.reserve(count * 2 * spine_len);
         for (size_t x = first; x < first + count; x++) {
-            const f4 lo = nodes[2 * x], hi = nodes[2 * x + 1];
-            out.push_back(lo);
-            out.push_back(hi);
-            uint32_t cl;
-            memcpy(&cl, &hi.w, 4);
-            if (cl & leaf_bit) {
-                out.push_back({0, 0, 0, 0});
-                out.push_back({0, 0, 0, 0});
-            } else {
-                uint32_t start;
+            size_t y = x;
+            bool live = true;
+            for (int j = 0; j < spine_len; j++) {
+                if (!live) {
+                    out.push_back({0, 0, 0, 0});
+                    out.push_back({0, 0, 0, 0});
+                    continue;
+                }
+                const f4 lo = nodes[2 * y], hi = nodes[2 * y + 1];
+                out.push_back(lo);
+                out.push_back(hi);
+                uint32_t cl, start;
+                memcpy(&cl, &hi.w, 4);
                 memcpy(&start, &lo.w, 4);
-                const size_t c1 = base + start + 1;
-                out.push_back(nodes[2 * c1]);
-                out.push_back(nodes[2 * c1 + 1]);
+                if (cl & leaf_bit)
+                    live = false;
+                else
+                    y = base + start + 1;
             }
         }
         return out;

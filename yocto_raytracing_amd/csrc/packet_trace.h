@@ -113,7 +113,7 @@ __device__ __forceinline__ const f4* sgpr_ptr(const f4* p) {
 
 template <int N>
 __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
-    static_assert(N == 2 || N == 3 || N == 4 || N == 8, "record count");
+    static_assert(N == 2 || N == 3 || N == 4 || N == 6 || N == 8, "record count");
     const f4* p = sgpr_ptr(p_);
     if constexpr (N == 2) {
         sgpr8 a;
@@ -130,6 +130,14 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, 0x0\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+    } else if constexpr (N == 6) {
+        sgpr16 a;
+        sgpr8 b;
+        asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx8 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
+                     : "=s"(a), "=s"(b)
+                     : "s"(p));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+        out[4] = rec_of(b, 0), out[5] = rec_of(b, 1);
     } else {
         sgpr16 a, b;
         asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx16 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
@@ -151,6 +159,43 @@ __device__ __forceinline__ void ld_records(const f4* p, float4 (&out)[N]) {
     ld_uniform<N>(p, out);
 #endif
 }
+
+// the same with the record index applied as an SGPR byte offset of the load itself
+// (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
+template <int N>
+__device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
+    static_assert(N == 4 || N == 8, "record count");
+    const f4* base = sgpr_ptr(base_);
+    const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
+    if constexpr (N == 4) {
+        sgpr16 a;
+        asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+    } else {
+        sgpr16 a, b;
+        asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                     : "=s"(a), "=s"(b)
+                     : "s"(base), "s"(off));
+#pragma unroll
+        for (int k = 0; k < 4; k++) out[k] = rec_of(a, k), out[4 + k] = rec_of(b, k);
+    }
+}
+
+#ifndef YRT_SOFF
+#define YRT_SOFF 1
+#endif
+// N records at base + index (16-byte units)
+template <int N>
+__device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, float4 (&out)[N]) {
+#if YRT_SCALAR_LOADS && YRT_SOFF
+    if constexpr (N == 4 || N == 8) {
+        ld_scalar_at<N>(base, index, out);
+        return;
+    }
+#endif
+    ld_records<N>(base + index, out);
+}
+
 
 // intersect_triangle (scene.cpp:229-263) without branches: the same values in the
 // same order; the early returns become one predicate (a NaN w1/w2/t passes its
@@ -195,66 +240,59 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
     unsigned long long inst_mask = 0;  // lanes entering the current instance leaf
     int level = 0, sp = 0, base = 0, root = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
     int node = 0;
-    // pair records of the current level (yrt_device.h tpair/spair): node X's record and
-    // that of its child start+1, so one fetch serves the two tests the reference makes
-    // back to back (test X; push start; pop start+1 and test it -- no primitive test
-    // and so no tmax change in between)
+    // spine records of the current level (yrt_device.h tpair/spair): node X's record and
+    // those of X's child start+1, its child start+1, ... -- the nodes the reference
+    // tests back to back (test X; push start; pop start+1 and test it; ...) with no
+    // primitive test, and so no tmax change, in between: one fetch serves them all
     const f4* pbase = S.tpair;
     unsigned long long mask = live;
     for (;;) {
-        // ---- every lane of `mask` tests `node` with its own ray ----
         node = uniform(node);  // keep the node index (and the address math) scalar
-        float4 rec[4];
-        ld_records<4>(pbase + 4 * node, rec);
-        const float4 lo = rec[0], hi = rec[1];
-        if (COUNT && (mask & me)) wc.box++;
+        float4 rec[2 * spine_len];
+        ld_records_at<2 * spine_len>(pbase, (unsigned)(2 * spine_len * node), rec);
+        bool pass[spine_len];
+#pragma unroll
+        for (int j = 0; j < spine_len; j++) pass[j] = box_hit(co, ci, tmin, tmax, rec[2 * j], rec[2 * j + 1]);
         if (COUNT && lane == 0) wc.wnode++;
-        const unsigned long long pm = ballot(box_hit(co, ci, tmin, tmax, lo, hi)) & mask;
-        // the child start+1, tested now with the same tmax (used only if X is inner and passes)
-        const bool pass1 = box_hit(co, ci, tmin, tmax, rec[2], rec[3]);
 #ifdef YRT_EXP_LAT  // diagnostic: one more dependent fetch per step
         {
             float4 again[2];
-            ld_records<2>(pbase + 4 * (node ^ (int)(pm & 1)), again);
+            ld_records<2>(pbase + 2 * spine_len * (node ^ (int)(mask & 1)), again);
             asm volatile("" ::"v"(again[0].x));
         }
 #endif
-        // the leaf to process after this step, if any: first slot, count|leaf, lanes
-        int lstart = 0;
-        uint32_t lcl = 0;
-        unsigned long long lmask = 0;
-        if (pm) {
-            const int start = uniform(ibits(lo.w));
-            const uint32_t cl = (uint32_t)uniform((int)ubits(hi.w));
-            if (!(cl & leaf_bit)) {
-                // push start (slot sp of the stack VGPRs := {start, pm}); the reference
-                // pops start+1 next and tests it: that is pass1
-                bool at = lane_now() == sp;
-                stk_node = at ? start : stk_node;
-                stk_mlo = at ? (int)(uint32_t)pm : stk_mlo;
-                stk_mhi = at ? (int)(uint32_t)(pm >> 32) : stk_mhi;
-                sp++;
-                if (COUNT && (pm & me)) wc.box++;
-                const unsigned long long p1 = ballot(pass1) & pm;
-                if (p1) {
-                    const int start1 = uniform(ibits(rec[2].w));
-                    const uint32_t cl1 = (uint32_t)uniform((int)ubits(rec[3].w));
-                    if (!(cl1 & leaf_bit)) {
-                        at = lane_now() == sp;
-                        stk_node = at ? start1 : stk_node;
-                        stk_mlo = at ? (int)(uint32_t)p1 : stk_mlo;
-                        stk_mhi = at ? (int)(uint32_t)(p1 >> 32) : stk_mhi;
-                        sp++;
-                        node = start1 + 1;
-                        mask = p1;
-                        continue;
-                    }
-                    lstart = start1, lcl = cl1, lmask = p1;
-                }
-            } else {
+        // walk down the spine: node j is tested by the lanes that passed node j-1
+        int lstart = 0;          // the leaf to process after this step, if any:
+        uint32_t lcl = 0;        //   first slot, count | leaf_bit,
+        unsigned long long lmask = 0;  //   lanes
+        bool descend = false;
+        unsigned long long mj = mask;
+#pragma unroll
+        for (int j = 0; j < spine_len; j++) {
+            if (COUNT && (mj & me)) wc.box++;
+            const unsigned long long pm = ballot(pass[j]) & mj;
+            if (!pm) break;
+            const int start = uniform(ibits(rec[2 * j].w));
+            const uint32_t cl = (uint32_t)uniform((int)ubits(rec[2 * j + 1].w));
+            if (cl & leaf_bit) {
                 lstart = start, lcl = cl, lmask = pm;
+                break;
+            }
+            // push start (slot sp of the stack VGPRs := {start, pm}); the reference pops
+            // start+1 next and tests it: that is spine node j+1
+            const bool at = lane_now() == sp;
+            stk_node = at ? start : stk_node;
+            stk_mlo = at ? (int)(uint32_t)pm : stk_mlo;
+            stk_mhi = at ? (int)(uint32_t)(pm >> 32) : stk_mhi;
+            sp++;
+            mj = pm;
+            if (j == spine_len - 1) {
+                node = start + 1;
+                mask = pm;
+                descend = true;
             }
         }
+        if (descend) continue;
         if (lmask) {
             const int start = lstart;
             const int count = (int)(lcl & 0xffffu);
@@ -297,7 +335,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     }
                     leaf_hit |= h ? 1 : 0;
                 }
-                hit |= leaf_hit;
+                if (ANY) hit |= leaf_hit;  // closest hit: hit == (hr.slot >= 0), nothing to carry
                 // any-hit lanes are finished; a NaN tmax fails every later slab test
                 done |= ballot(ANY ? leaf_hit : (leaf_hit && is_nan(tmax)));
                 if (ANY && !(live & ~done)) return hit;
@@ -320,7 +358,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     const uint32_t rk = (uint32_t)uniform(ibits(fo.w));
                     root = (int)(rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
-                    pbase = S.spair + 4 * root;
+                    pbase = S.spair + 2 * spine_len * root;
                     cur_slot = k;
                     node = 0;  // the shape root, tested like any popped node
                     mask = inst_mask & ~done;
@@ -335,9 +373,11 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                 ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
             }
             if (sp == 0) {
-                if (!ANY && hit) {
+                if (!ANY) {
+                    if (hr.slot < 0) return false;
                     hr.ew = {1 - hw1 - hw2, hw1, hw2, 0};
                     hr.dist = tmax;
+                    return true;
                 }
                 return hit;
             }
@@ -400,7 +440,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
         if (!(info & leaf_bit)) {
             WSTAT(0);
             float4 r[8];
-            ld_records<8>(S.wnodes + 8 * ref, r);
+            ld_records_at<8>(S.wnodes, (unsigned)(8 * ref), r);
             const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
                         lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
                         hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
@@ -485,7 +525,7 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
                     WSTAT(3);
                     const int k = inst_next++;
                     float4 fr[4];
-                    ld_records<4>(S.tinst + 4 * k, fr);
+                    ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
                     cd = transform_direction_inverse(f, wd);

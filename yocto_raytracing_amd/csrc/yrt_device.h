@@ -42,6 +42,10 @@ enum shape_kind : int { kind_triangles = 0, kind_lines = 1, kind_points = 2, kin
 enum mat_flags : int { mat_reflective = 1 };
 
 constexpr uint32_t leaf_bit = 0x80000000u;
+#ifndef YRT_SPINE
+#define YRT_SPINE 2
+#endif
+constexpr int spine_len = YRT_SPINE;  // nodes per closest-hit walk record (2..4)
 
 struct dev_scene_view {
     const f4* tnodes;
@@ -59,7 +63,8 @@ struct dev_scene_view {
     const i4* texinfo;
     const float* srgb;
     const f4* wnodes;
-    const f4* tpair;  // 4 x f4 per instance-BVH node: its record + its child start+1's
+    const f4* tpair;  // 2*spine_len x f4 per instance-BVH node: its record, then its
+                      // child start+1's, that child's start+1's, ... (right spine)
     const f4* spair;  // the same for the shape BVHs (same indexing as snodes)
     const int* tinst_id;
     int wtop_root;
