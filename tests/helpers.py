@@ -154,3 +154,14 @@ def read_png_rgba8(path) -> np.ndarray:
     raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, w * 4 + 1)
     assert (raw[:, 0] == 0).all(), "unexpected PNG row filter"
     return raw[:, 1:].reshape(h, w, 4)
+
+
+def assert_same_floats(got, want):
+    """bit-for-bit equality, except that a NaN only has to be a NaN: its sign and
+    payload follow the GPU's NaN propagation, not x86's"""
+    got = np.asarray(got, np.float32)
+    want = np.asarray(want, np.float32)
+    assert got.shape == want.shape
+    gn, wn = np.isnan(got), np.isnan(want)
+    np.testing.assert_array_equal(gn, wn)
+    np.testing.assert_array_equal(got[~gn].view(np.uint32), want[~wn].view(np.uint32))

@@ -9,7 +9,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from helpers import GOLDEN, ROOT, SCENE_NAMES, Oracle, digests, have_reference, scene_path
+from helpers import GOLDEN, ROOT, SCENE_NAMES, Oracle, assert_same_floats, digests, have_reference, scene_path
 
 
 @pytest.mark.parametrize("name", SCENE_NAMES)
@@ -82,3 +82,19 @@ def test_oracle_vs_live_reference(name, res, spp):
     img, nrays, _ = Oracle(name).render(res, spp)
     assert nrays == n
     np.testing.assert_array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["basic", "refl", "instance10000", "lines"])
+def test_oracle_trace_degenerate_rays_vs_reference(name):
+    """axis-parallel rays (0*inf slabs), rays on box planes, NaN/inf/zero components,
+    empty and inverted [tmin, tmax]: the reference's answers (make_degenerate.py)"""
+    z = np.load(GOLDEN / f"ref_rays_degenerate_{name}.npz")
+    o = Oracle(name)
+    got = o.trace(z["rays"])
+    np.testing.assert_array_equal(got["hit"], z["hit"].astype(bool))
+    h = z["hit"] > 0
+    np.testing.assert_array_equal(got["ei"][h], z["ei"][h])
+    np.testing.assert_array_equal(got["inst"][h], z["inst"][h])
+    assert_same_floats(got["ew"][h], z["ew"][h])
+    assert_same_floats(got["dist"][h], z["dist"][h])
+    np.testing.assert_array_equal(o.trace(z["rays"], any_hit=True)["hit"], z["any_hit"].astype(bool))
