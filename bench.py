@@ -5,7 +5,8 @@ MI355X GPUs of one node.
 One step = one full frame of the hot path (raytrace(), src/raytrace.cpp:213) over
 the resident scene, end to end: every rank renders its interleaved 8-row bands of
 the frame with the gfx950 kernel, then the float framebuffer is all-gathered over
-RCCL (xGMI) and rank 0 reassembles the image (the north_star's framebuffer gather).
+RCCL (xGMI) and every rank reassembles the image (the north_star's framebuffer gather);
+with RCCL the gather of frame i runs on a communication stream while frame i+1 renders.
 Total work is fixed as N grows ("scaling": "strong").
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -160,11 +161,20 @@ def main():
     band, local_rows = render_params_band(layout, rank)
     params.band, params.band_stride, params.band_offset = band
     params.tile_h = local_rows  # every rank renders the same padded count (rows past H read 0)
-    shard = torch.empty((local_rows, W, 4), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    # two frames in flight at N > 1 over RCCL: frame i's all_gather + reassembly run on a
+    # communication stream while frame i+1 renders (double-buffered shards and frames)
+    overlap = world > 1 and (dist.get_backend() == "nccl" or os.environ.get("YRT_BENCH_OVERLAP") == "1")
+    nbuf = 2 if overlap else 1
+    shards = [torch.empty((local_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    gathered = [torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+                for _ in range(nbuf)]
+    frames = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    shard = shards[0]
     index = torch.as_tensor(layout.gather_index(), device=dev)
-    frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev) if overlap else None
+    rendered = [torch.cuda.Event() for _ in range(nbuf)]
+    gathered_ev = [None] * nbuf
 
     # untimed instrumented pass: algorithmic work counts for the roofline bytes
     pc = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=band, count_work=True,
@@ -193,21 +203,33 @@ def main():
     if a.algorithm == "wavefront":  # the timed shadow kernel walks the 4-wide collapse
         kernel_names["shadow"] = "k_shadow<false, true, unsigned int, true>"
 
-    def step(timing=0):
+    def step(i, timing=0):
+        b = i % nbuf
         params.timing = timing
-        ds.render_into(params, shard.data_ptr(), stream=stream.cuda_stream)
-        gather_frame(shard, layout, index, gathered, frame)
+        if not overlap:
+            ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
+            gather_frame(shards[b], layout, index, gathered[b], frames[b])
+            return
+        if gathered_ev[b] is not None:  # shards[b] is free once its previous gather has read it
+            stream.wait_event(gathered_ev[b])
+        ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
+        rendered[b].record(stream)
+        with torch.cuda.stream(comm):
+            comm.wait_event(rendered[b])
+            gather_frame(shards[b], layout, index, gathered[b], frames[b])
+            gathered_ev[b] = torch.cuda.Event()
+            gathered_ev[b].record(comm)
 
-    for _ in range(a.warmup):
-        step()
+    for i in range(a.warmup):
+        step(i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         # HIP events around every kernel launch, on the launch stream (library-side)
-        step(timing=1 if i == 0 else 2)
-    torch.cuda.synchronize(dev)
+        step(i, timing=1 if i == 0 else 2)
+    torch.cuda.synchronize(dev)  # every stream of the device: renders and gathers
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -254,7 +276,9 @@ def main():
             "data": "in/instance10000_pointlight scene (reference input, .yrtscene); deterministic camera samples",
             "config": {"workload": f"{a.scene} {W}x{H} {a.samples}x{a.samples} spp, amb 0.1, one frame per step",
                        "scene": a.scene, "width": W, "height": H, "spp": a.samples * a.samples,
-                       "parallelism": f"image bands x{world} + RCCL all_gather" if world > 1 else "single GPU",
+                       "parallelism": (f"image bands x{world} + RCCL all_gather" +
+                                       (" overlapped with the next frame" if overlap else "")) if world > 1
+                       else "single GPU",
                        "rays_per_frame": total_rays / a.steps,
                        "camera_samples_per_frame": total_samples / a.steps,
                        "gpu_ms_per_frame": render_ms,
