@@ -30,7 +30,7 @@ def main(argv):
         for src in b.SOURCES:  # host and device code both see the defines
             o = vdir / (Path(src).stem + ".o")
             if src.endswith(".hip"):
-                cmd = [b.HIPCC, *b.COMMON, *defines, f"--offload-arch={b.ARCH}", "-c", str(b.CSRC / src), "-o", str(o)]
+                cmd = [b.HIPCC, *b.COMMON, *b.DEVICE_FLAGS, *defines, f"--offload-arch={b.ARCH}", "-c", str(b.CSRC / src), "-o", str(o)]
             else:
                 cmd = [b.CLANGXX, *b.COMMON, *b.HOST_DEFS, *defines, "-c", str(b.CSRC / src), "-o", str(o)]
             subprocess.run(cmd, check=True, capture_output=True)

@@ -444,6 +444,12 @@ device_scene* device_scene_create(const scene& scn, int device) {
     ds->nsnodes = snodes.size() / 2;
     ds->nsprims = sprims.size() / 3;
     ds->ninst = tinst.size() / 4;
+#ifdef YRT_DEBUG_BOUNDS
+    v.nsnodes = (int)ds->nsnodes;
+    v.nsprims = (int)ds->nsprims;
+    v.ninst = (int)ds->ninst;
+    v.nwnodes = (int)wnodes.size() / 8;
+#endif
     return ds;
 }
 

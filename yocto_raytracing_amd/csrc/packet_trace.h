@@ -52,6 +52,10 @@ __device__ __forceinline__ int lane_now() {
     return l;
 }
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+// v_writelane_b32 (the LLVM intrinsic; clang has no builtin for it): value -> lane `lane`
+// of `old`, every other lane kept; exec is ignored
+extern "C" __device__ int yrt_llvm_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ int writelane(int old, int value, int lane) { return yrt_llvm_writelane(value, lane, old); }
 __device__ __forceinline__ float lane_value(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -95,6 +99,9 @@ __device__ __forceinline__ void ld_uniform(const f4* p, float4 (&out)[N]) {
 // cache into SGPRs (s_load_dwordx4/x8/x16; the scene is read-only for the whole
 // launch). The VALU reads them as scalar operands; nothing occupies the vector memory
 // pipe, which a 64-lane load of one shared address would (1 KiB returned per record).
+// Where one asm block issues two loads its outputs are early-clobber ("=&s"): the
+// first load's destination must not share registers with the address the second one
+// reads, or a quickly returning first load overwrites it (an intermittent fault).
 typedef int sgpr4 __attribute__((ext_vector_type(4)));
 typedef int sgpr8 __attribute__((ext_vector_type(8)));
 typedef int sgpr16 __attribute__((ext_vector_type(16)));
@@ -123,7 +130,7 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
         sgpr8 a;
         sgpr4 b;
         asm volatile("s_load_dwordx8 %0, %2, 0x0\n s_load_dwordx4 %1, %2, 0x20\n s_waitcnt lgkmcnt(0)"
-                     : "=s"(a), "=s"(b)
+                     : "=&s"(a), "=&s"(b)
                      : "s"(p));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(b, 0);
     } else if constexpr (N == 4) {
@@ -134,14 +141,14 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
         sgpr16 a;
         sgpr8 b;
         asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx8 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
-                     : "=s"(a), "=s"(b)
+                     : "=&s"(a), "=&s"(b)
                      : "s"(p));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
         out[4] = rec_of(b, 0), out[5] = rec_of(b, 1);
     } else {
         sgpr16 a, b;
         asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx16 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
-                     : "=s"(a), "=s"(b)
+                     : "=&s"(a), "=&s"(b)
                      : "s"(p));
 #pragma unroll
         for (int k = 0; k < 4; k++) out[k] = rec_of(a, k), out[4 + k] = rec_of(b, k);
@@ -174,7 +181,7 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
     } else {
         sgpr16 a, b;
         asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                     : "=s"(a), "=s"(b)
+                     : "=&s"(a), "=&s"(b)
                      : "s"(base), "s"(off));
 #pragma unroll
         for (int k = 0; k < 4; k++) out[k] = rec_of(a, k), out[4 + k] = rec_of(b, k);
@@ -392,6 +399,197 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
 }
 
 
+#ifdef YRT_DEBUG_BOUNDS
+// diagnostic build: the first out-of-range walk state is recorded here (no fault; the
+// walk gives up): {code, a, b, c, d, e}
+static __device__ unsigned g_dbg_bounds[8];
+__device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int d, int e) {
+    if ((__lane_id() == 0) && atomicCAS(&g_dbg_bounds[0], 0u, code) == 0u) {
+        g_dbg_bounds[1] = a, g_dbg_bounds[2] = b, g_dbg_bounds[3] = c, g_dbg_bounds[4] = d, g_dbg_bounds[5] = e;
+    }
+    return true;
+}
+#define DBG_CHECK(cond, code, a, b, c, d, e) \
+    if (!(cond) && dbg_fail(code, a, b, c, d, e)) return false
+#else
+#define DBG_CHECK(cond, code, a, b, c, d, e)
+#endif
+
+// ---- closest hit, laid out for the scalar unit ----
+// The same walk as packet_trace<false> (same node tests, in the same order, with the
+// same tmax per lane), with the control flow written as explicit states joined by
+// gotos so that the hot descent path carries no merged loop state: per spine node
+// one s_and (ballot & mask, SCC = any lane), one leaf test and one stack push. The
+// push is three v_writelane of the SGPR values into lane sp of the stack VGPRs (no
+// lane-index compare, no selects). SALU issue -- one scalar unit per CU shared by
+// its four SIMDs -- is what bounds the closest-hit kernels (SQ_INSTS_SALU per CU
+// against the kernel's cycles), so every scalar instruction on the descent counts.
+template <bool COUNT>
+__device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
+                                             work_counts& wc) {
+    static_assert(spine_len == 2, "packet_first walks two-node spine records");
+    const unsigned long long me = 1ull << __lane_id();
+    const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
+    if (!live) return false;
+    const vec3f wo = wray.o, wd = wray.d;
+    const float tmin = wray.tmin;
+    float tmax = wray.tmax;
+    vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    float hw1 = 0, hw2 = 0;
+    int hslot = -1, hei = -1;
+    int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
+    unsigned long long done = 0, inst_mask = 0, mask = live;
+    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
+    int node = 0;
+    const f4* pbase = S.tpair;
+    for (;;) {
+        // ---- descent: one spine record per step, until a leaf or no passing lane ----
+        unsigned long long lmask = 0;
+        int lstart = 0, lcount = 0;
+        for (;;) {
+            DBG_CHECK(node >= 0 && sp >= 0 && sp < 63 &&
+                          (level == 0 ? node < S.ntnodes : (int)((pbase - S.spair) / 4) + node < S.nsnodes),
+                      1, node, sp, level, (int)((pbase - S.spair) / 4), base);
+            float4 rec[4];
+            ld_records_at<4>(pbase, (unsigned)(4 * node), rec);
+            const bool p0 = box_hit(co, ci, tmin, tmax, rec[0], rec[1]);
+            const bool p1 = box_hit(co, ci, tmin, tmax, rec[2], rec[3]);
+            if (COUNT && (me & 1)) wc.wnode++;
+            if (COUNT && (mask & me)) wc.box++;
+            const unsigned long long pm0 = ballot(p0) & mask;
+            if (!pm0) break;
+            const int s0 = uniform(ibits(rec[0].w));
+            const uint32_t c0 = (uint32_t)uniform(ibits(rec[1].w));
+            if (c0 & leaf_bit) {
+                lstart = s0, lcount = (int)(c0 & 0xffffu), lmask = pm0;
+                break;
+            }
+            // push start; the reference pops start+1 next and tests it: spine node 1
+            stk_node = writelane(stk_node, s0, sp);
+            stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
+            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
+            sp++;
+            if (COUNT && (pm0 & me)) wc.box++;
+            const unsigned long long pm1 = ballot(p1) & pm0;
+            if (!pm1) break;
+            const int s1 = uniform(ibits(rec[2].w));
+            const uint32_t c1 = (uint32_t)uniform(ibits(rec[3].w));
+            if (c1 & leaf_bit) {
+                lstart = s1, lcount = (int)(c1 & 0xffffu), lmask = pm1;
+                break;
+            }
+            stk_node = writelane(stk_node, s1, sp);
+            stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
+            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
+            sp++;
+            node = s1 + 1;
+            mask = pm1;
+        }
+        // ---- the leaf reached, if any ----
+        if (lmask) {
+            if (level == 0) {
+                inst_next = lstart;
+                inst_end = lstart + lcount;
+                inst_mask = lmask;
+                level = 1;
+                base = sp;
+            } else {
+                const bool in = (lmask & me) != 0;
+                int leaf_hit = 0;
+                DBG_CHECK(lstart >= 0 && lstart + lcount <= S.nsprims, 2, lstart, lcount, level, kind, sp);
+                if (kind == kind_triangles) {
+                    for (int i = lstart; i < lstart + lcount; i++) {
+                        float4 pv[3];
+                        ld_records<3>(S.sprims + 3 * i, pv);
+                        if (COUNT && in) wc.prim++;
+                        if (COUNT && (me & 1)) wc.wprim++;
+                        float t, w1, w2;
+                        const bool h =
+                            tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2) && in;
+                        tmax = h ? t : tmax;
+                        hslot = h ? cur_slot : hslot;
+                        hei = h ? ibits(pv[0].w) : hei;
+                        hw1 = h ? w1 : hw1;
+                        hw2 = h ? w2 : hw2;
+                        leaf_hit |= h ? 1 : 0;
+                    }
+                } else {
+                    for (int i = lstart; i < lstart + lcount; i++) {
+                        float4 pv[3];
+                        ld_records<3>(S.sprims + 3 * i, pv);
+                        if (COUNT && in) wc.prim++;
+                        if (COUNT && (me & 1)) wc.wprim++;
+                        // lines: ew = {1-s, s, 0, 0}; points: {1, 0, 0, 0} -- both are
+                        // {1-w1-w2, w1, w2, 0} with w1 = ew.y, w2 = ew.z
+                        float t;
+                        vec4f ew;
+                        const ray3 lr = {co, cd, tmin, tmax};
+                        bool h = kind == kind_lines ? line_hit(lr, xyz(pv[0]), xyz(pv[1]), pv[1].w, pv[2].x, t, ew)
+                                                    : point_hit(lr, xyz(pv[0]), pv[1].x, t, ew);
+                        h = h && in;
+                        tmax = h ? t : tmax;
+                        hslot = h ? cur_slot : hslot;
+                        hei = h ? ibits(pv[0].w) : hei;
+                        hw1 = h ? ew.y : hw1;
+                        hw2 = h ? ew.z : hw2;
+                        leaf_hit |= h ? 1 : 0;
+                    }
+                }
+                // a NaN tmax fails every later slab test: such a lane leaves the walk
+                done |= ballot(leaf_hit && is_nan(tmax));
+            }
+        }
+        // ---- the next node: the next instance of the current leaf, or a pop ----
+        bool finished = false;
+        for (;;) {
+            if (level == 1 && sp == base) {
+                if (inst_next < inst_end) {
+                    // enter instance k: transform_ray_inverse (vmath.h:275-278), every lane
+                    const int k = inst_next++;
+                    DBG_CHECK(k >= 0 && k < S.ninst, 3, k, inst_end, sp, base, 0);
+                    float4 fr[4];
+                    ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
+                    const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
+                    co = transform_point_inverse(f, wo);
+                    cd = transform_direction_inverse(f, wd);
+                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    const uint32_t rk = (uint32_t)uniform(ibits(fr[3].w));
+                    pbase = S.spair + 2 * spine_len * (rk & 0x3fffffffu);
+                    kind = (int)(rk >> 30);
+                    cur_slot = k;
+                    mask = inst_mask & ~done;
+                    if (COUNT && (mask & me)) wc.inst++;
+                    node = 0;  // the shape root, tested like any popped node
+                    if (mask) break;
+                    continue;
+                }
+                level = 0;
+                pbase = S.tpair;
+                co = wo;
+                cd = wd;
+                ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+            }
+            if (sp == 0) {
+                finished = true;
+                break;
+            }
+            sp--;
+            node = __builtin_amdgcn_readlane(stk_node, sp);
+            mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
+                    (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
+                   ~done;
+            if (mask) break;
+        }
+        if (finished) break;
+    }
+    if (hslot < 0) return false;
+    hr.slot = hslot;
+    hr.ei = hei;
+    hr.ew = {1 - hw1 - hw2, hw1, hw2, 0};
+    hr.dist = tmax;
+    return true;
+}
+
 #ifndef YRT_WIDE_HOIST
 #define YRT_WIDE_HOIST 0  // 1: slab-swap signs hoisted to level changes (A/B: +2 %)
 #endif
@@ -556,6 +754,149 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
             if (mask) break;
         }
     }
+}
+
+// ---- any hit on the 4-wide collapse, laid out for the scalar unit ----
+// packet_occluded_wide's walk (same wide nodes, same push order, same leaves) with
+// packet_first's structure: a single-exit descent loop over wide nodes, the leaf,
+// then the pop loop; pushes are v_writelane of the SGPR values into lane sp.
+__device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid) {
+    const unsigned long long me = 1ull << __lane_id();
+    const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
+    if (!live) return false;
+    const vec3f wo = wray.o, wd = wray.d;
+    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    const float tmin = wray.tmin, tmax = wray.tmax;
+    vec3f co = wo, cd = wd, ci = wi;
+    int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
+    unsigned long long done = 0, inst_mask = 0;
+    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
+    // the current item: a wide node (info 1) or a leaf (info = count | leaf_bit)
+    int ref = S.wtop_root;
+    uint32_t info = 1;
+    unsigned long long mask = live;
+    for (;;) {
+        // ---- descent through wide nodes until a leaf or no passing child ----
+        while (!(info & leaf_bit)) {
+            DBG_CHECK(ref >= 0 && ref < S.nwnodes && sp >= 0 && sp < 61, 4, ref, sp, level, base, 0);
+            float4 r[8];
+            ld_records_at<8>(S.wnodes, (unsigned)(8 * ref), r);
+            const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
+                        lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
+                        hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
+            const int rf[4] = {uniform(ibits(r[6].x)), uniform(ibits(r[6].y)), uniform(ibits(r[6].z)),
+                               uniform(ibits(r[6].w))};
+            const int in[4] = {uniform(ibits(r[7].x)), uniform(ibits(r[7].y)), uniform(ibits(r[7].z)),
+                               uniform(ibits(r[7].w))};
+            unsigned long long m[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float tn;
+                m[k] = 0;
+                // empty slots (info 0) are skipped on a scalar branch
+                if (in[k] != 0) m[k] = ballot(box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)) & mask;
+            }
+            int first = -1;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (!m[k]) continue;
+                if (first < 0) {
+                    first = k;
+                    continue;
+                }
+                stk_ref = writelane(stk_ref, rf[k], sp);
+                stk_info = writelane(stk_info, in[k], sp);
+                stk_mlo = writelane(stk_mlo, (int)(uint32_t)m[k], sp);
+                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m[k] >> 32), sp);
+                sp++;
+            }
+            if (first < 0) {
+                mask = 0;
+                break;
+            }
+            ref = first == 0 ? rf[0] : first == 1 ? rf[1] : first == 2 ? rf[2] : rf[3];
+            info = (uint32_t)(first == 0 ? in[0] : first == 1 ? in[1] : first == 2 ? in[2] : in[3]);
+            mask = first == 0 ? m[0] : first == 1 ? m[1] : first == 2 ? m[2] : m[3];
+        }
+        // ---- the leaf reached, if any ----
+        if (mask) {
+            if (level == 0) {
+                inst_next = ref;
+                inst_end = ref + (int)(info & 0xffffu);
+                inst_mask = mask;
+                level = 1;
+                base = sp;
+            } else {
+                const bool inl = (mask & me) != 0;
+                int leaf_hit = 0;
+                const int count = (int)(info & 0xffffu);
+                DBG_CHECK(ref >= 0 && ref + count <= S.nsprims, 5, ref, count, level, kind, sp);
+                if (kind == kind_triangles) {
+                    for (int i = ref; i < ref + count; i++) {
+                        float4 pv[3];
+                        ld_records<3>(S.sprims + 3 * i, pv);
+                        float t, w1, w2;
+                        const bool h = tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2);
+                        leaf_hit |= (h && inl) ? 1 : 0;
+                    }
+                } else {
+                    for (int i = ref; i < ref + count; i++) {
+                        float4 pv[3];
+                        ld_records<3>(S.sprims + 3 * i, pv);
+                        float t;
+                        vec4f ew;
+                        const ray3 lr = {co, cd, tmin, tmax};
+                        const bool h = kind == kind_lines
+                                           ? line_hit(lr, xyz(pv[0]), xyz(pv[1]), pv[1].w, pv[2].x, t, ew)
+                                           : point_hit(lr, xyz(pv[0]), pv[1].x, t, ew);
+                        leaf_hit |= (h && inl) ? 1 : 0;
+                    }
+                }
+                done |= ballot(leaf_hit != 0);
+                if (!(live & ~done)) break;
+            }
+        }
+        // ---- the next item: the next instance of the current leaf, or a pop ----
+        bool finished = false;
+        for (;;) {
+            if (level == 1 && sp == base) {
+                if (inst_next < inst_end) {
+                    const int k = inst_next++;
+                    DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_end, sp, base, 0);
+                    float4 fr[4];
+                    ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
+                    const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
+                    co = transform_point_inverse(f, wo);
+                    cd = transform_direction_inverse(f, wd);
+                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
+                    ref = (int)(rk & 0x3fffffffu);
+                    kind = (int)(rk >> 30);
+                    info = 1;
+                    mask = inst_mask & ~done;
+                    if (mask) break;
+                    continue;
+                }
+                level = 0;
+                co = wo;
+                cd = wd;
+                ci = wi;
+            }
+            if (sp == 0) {
+                finished = true;
+                break;
+            }
+            sp--;
+            ref = __builtin_amdgcn_readlane(stk_ref, sp);
+            info = (uint32_t)__builtin_amdgcn_readlane(stk_info, sp);
+            mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
+                    (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
+                   ~done;
+            if (mask) break;
+        }
+        if (finished) break;
+    }
+    return (done & me) != 0;
 }
 
 }  // namespace yrt

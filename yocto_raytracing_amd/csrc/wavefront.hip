@@ -41,6 +41,9 @@ constexpr int WF_BLOCK = 256;
 #ifndef YRT_EXP_SHADOW_LDS
 #define YRT_EXP_SHADOW_LDS 0  // experiment knob: dynamic LDS per shadow block (occupancy cap)
 #endif
+#ifndef YRT_PF2
+#define YRT_PF2 1  // closest hit: packet_first (goto-structured walk) instead of packet_trace<false>
+#endif
 constexpr int MAX_LEVELS = 16;
 constexpr int TILE = 8;  // pixel tiles of 8x8 in the sample enumeration
 
@@ -144,7 +147,12 @@ struct tracer {
     SE* lane_stk;
     __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
                                           work_counts& wc) {
-        if (PACKET) return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
+        if (PACKET) {
+#if YRT_PF2
+            if constexpr (!ANY) return packet_first<COUNT>(S, ray, valid, hr, wc);
+#endif
+            return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
+        }
         if (!valid) return false;
         if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
         return traverse<false, COUNT, WF_BLOCK>(S, ray, hr, lane_stk, wc);
@@ -282,7 +290,11 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_shadow(dev_scene_
         hit_record hr;
         bool occ;
         if constexpr (WIDE)
+#if YRT_PF2
+            occ = packet_occluded_wide2(S, sr, valid);
+#else
             occ = packet_occluded_wide(S, sr, valid);
+#endif
         else
             occ = T.trace(S, sr, valid, hr, wc);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
@@ -637,6 +649,17 @@ hipError_t launch_render_wavefront(device_scene& ds, const dev_render_args& args
 }
 
 }  // namespace yrt
+
+#ifdef YRT_DEBUG_BOUNDS
+extern "C" int yrt_debug_bounds(unsigned* out8, int reset) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(yrt::g_dbg_bounds), 8 * sizeof(unsigned)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned z[8] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_dbg_bounds), z, sizeof z);
+    }
+    return 0;
+}
+#endif
 
 #ifdef YRT_WIDE_STATS
 extern "C" int yrt_debug_wide_stats(unsigned long long* out8, int reset) {

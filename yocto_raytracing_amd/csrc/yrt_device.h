@@ -71,6 +71,9 @@ struct dev_scene_view {
     int wide;  // 1: any-hit queries use the 4-wide walk
     int nlights;
     int ntnodes;
+#ifdef YRT_DEBUG_BOUNDS  // diagnostic build: array sizes for the walks' bounds checks
+    int nsnodes, nsprims, ninst, nwnodes;
+#endif
 };
 
 // per-frame camera constants, hoisted from eval_camera (raytrace.cpp:16-24); tanf is
