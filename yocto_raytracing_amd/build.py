@@ -33,9 +33,10 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unus
 
 
 HOST_DEFS = ["-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
-# extra device-code flags (A/B knob). Not used: -structurizecfg-skip-uniform-regions
-# took 2-4 % off the walks but the build faulted on a 720p render.
-DEVICE_FLAGS: list = []
+# device code: leave wave-uniform regions unstructurized. Every branch of the BVH walks
+# is on an SGPR value; structurizing them adds flow variables and exec-mask juggling
+# (SALU) to every traversal step (A/B at c4: primary -2 %, shadow -4 %).
+DEVICE_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=true"]
 
 
 def _headers():
