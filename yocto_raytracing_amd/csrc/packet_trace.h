@@ -756,29 +756,50 @@ __device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, co
     }
 }
 
-// ---- any hit on the 4-wide collapse, laid out for the scalar unit ----
-// packet_occluded_wide's walk (same wide nodes, same push order, same leaves) with
-// packet_first's structure: a single-exit descent loop over wide nodes, the leaf,
-// then the pop loop; pushes are v_writelane of the SGPR values into lane sp.
-__device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid) {
-    const unsigned long long me = 1ull << __lane_id();
-    const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
-    if (!live) return false;
-    const vec3f wo = wray.o, wd = wray.d;
-    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
-    const float tmin = wray.tmin, tmax = wray.tmax;
-    vec3f co = wo, cd = wd, ci = wi;
-    int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
-    unsigned long long done = 0, inst_mask = 0;
-    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
-    // the current item: a wide node (info 1) or a leaf (info = count | leaf_bit)
-    int ref = S.wtop_root;
-    uint32_t info = 1;
-    unsigned long long mask = live;
-    for (;;) {
-        // ---- descent through wide nodes until a leaf or no passing child ----
+#ifndef YRT_WIDE_OCTANT
+#define YRT_WIDE_OCTANT 1  // wave-uniform slab signs: near/far planes picked at compile time
+#endif
+
+// intersect_check_bbox (scene.cpp:371-382) with the per-axis swap decided at compile
+// time: OCT bit a set = this lane's invd component a is < 0 (the reference's swap
+// condition). The same two products per axis are computed -- (lo - o) * invd and
+// (hi - o) * invd -- and each lands where the reference's swap puts it, so the values
+// are bit-identical; OCT 8 is the run-time select of box_hit6.
+template <int OCT>
+__device__ __forceinline__ bool box_oct(vec3f o, vec3f invd, float tmin_r, float tmax_r, float lx, float ly, float lz,
+                                        float hx, float hy, float hz) {
+    if constexpr (OCT == 8) {
+        float tn;
+        return box_hit6(o, invd, tmin_r, tmax_r, lx, ly, lz, hx, hy, hz, tn);
+    } else {
+        const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
+        const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
+        const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
+        const float t0x = (nx - o.x) * invd.x, t0y = (ny - o.y) * invd.y, t0z = (nz - o.z) * invd.z;
+        const float t1x = (fx - o.x) * invd.x, t1y = (fy - o.y) * invd.y, t1z = (fz - o.z) * invd.z;
+        float tmin = fmaxf(fmaxf(fmaxf(t0x, t0y), t0z), tmin_r);
+        float tmax = fminf(fminf(fminf(t1x, t1y), t1z), tmax_r);
+        tmax *= 1.00000024f;
+        return tmin <= tmax;
+    }
+}
+
+// the octant shared by every lane of `lanes` (bit a: invd component a < 0), or 8
+__device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes) {
+    const unsigned long long nx = ballot(invd.x < 0) & lanes, ny = ballot(invd.y < 0) & lanes,
+                             nz = ballot(invd.z < 0) & lanes;
+    if ((nx && nx != lanes) || (ny && ny != lanes) || (nz && nz != lanes)) return 8;
+    return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
+}
+
+// one descent of the 4-wide any-hit walk: wide nodes from `ref` until a leaf is the
+// current item (mask != 0) or no child passes (mask = 0); the passing children after
+// the first are pushed (v_writelane into lane sp of the stack VGPRs)
+template <int OCT>
+__device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, vec3f ci, float tmin, float tmax,
+                                             int& ref, uint32_t& info, unsigned long long& mask, int& sp,
+                                             int& stk_ref, int& stk_info, int& stk_mlo, int& stk_mhi) {
         while (!(info & leaf_bit)) {
-            DBG_CHECK(ref >= 0 && ref < S.nwnodes && sp >= 0 && sp < 61, 4, ref, sp, level, base, 0);
             float4 r[8];
             ld_records_at<8>(S.wnodes, (unsigned)(8 * ref), r);
             const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
@@ -791,10 +812,9 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             unsigned long long m[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                float tn;
                 m[k] = 0;
                 // empty slots (info 0) are skipped on a scalar branch
-                if (in[k] != 0) m[k] = ballot(box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)) & mask;
+                if (in[k] != 0) m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
             }
             int first = -1;
 #pragma unroll
@@ -818,6 +838,47 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             info = (uint32_t)(first == 0 ? in[0] : first == 1 ? in[1] : first == 2 ? in[2] : in[3]);
             mask = first == 0 ? m[0] : first == 1 ? m[1] : first == 2 ? m[2] : m[3];
         }
+}
+
+// ---- any hit on the 4-wide collapse, laid out for the scalar unit ----
+// packet_occluded_wide's walk (same wide nodes, same push order, same leaves) with
+// packet_first's structure: a single-exit descent loop over wide nodes, the leaf,
+// then the pop loop; pushes are v_writelane of the SGPR values into lane sp.
+__device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid) {
+    const unsigned long long me = 1ull << __lane_id();
+    const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
+    if (!live) return false;
+    const vec3f wo = wray.o, wd = wray.d;
+    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    const float tmin = wray.tmin, tmax = wray.tmax;
+    vec3f co = wo, cd = wd, ci = wi;
+    int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
+    unsigned long long done = 0, inst_mask = 0;
+    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
+    // the current item: a wide node (info 1) or a leaf (info = count | leaf_bit)
+    int ref = S.wtop_root;
+    uint32_t info = 1;
+    unsigned long long mask = live;
+    // the octant of the current level's rays when the whole wave shares it (8: mixed)
+    const int woct = YRT_WIDE_OCTANT ? wave_octant(wi, live) : 8;
+    int oct = woct;
+    for (;;) {
+        // ---- descent through wide nodes until a leaf or no passing child ----
+#if YRT_WIDE_OCTANT
+        switch (oct) {
+            case 0: wide_descend<0>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 1: wide_descend<1>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 2: wide_descend<2>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 3: wide_descend<3>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 4: wide_descend<4>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 5: wide_descend<5>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 6: wide_descend<6>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            case 7: wide_descend<7>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+            default: wide_descend<8>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
+        }
+#else
+        wide_descend<8>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi);
+#endif
         // ---- the leaf reached, if any ----
         if (mask) {
             if (level == 0) {
@@ -874,6 +935,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     kind = (int)(rk >> 30);
                     info = 1;
                     mask = inst_mask & ~done;
+                    if (YRT_WIDE_OCTANT) oct = wave_octant(ci, live & ~done);
                     if (mask) break;
                     continue;
                 }
@@ -881,6 +943,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 co = wo;
                 cd = wd;
                 ci = wi;
+                oct = woct;
             }
             if (sp == 0) {
                 finished = true;

@@ -36,7 +36,10 @@ namespace {
 
 constexpr int WF_BLOCK = 256;
 #ifndef YRT_TRACE_WAVES
-#define YRT_TRACE_WAVES 7  // waves per SIMD the traversal kernels are register-budgeted for (A/B: 6 -> 7 is -5 %, 8 spills too much)
+#define YRT_TRACE_WAVES 8  // waves per SIMD the traversal kernels are register-budgeted for (A/B at c4 with the structured walks: 7 -> 8 is -3.5 %)
+#endif
+#ifndef YRT_SHADOW_WAVES
+#define YRT_SHADOW_WAVES YRT_TRACE_WAVES  // the same for k_shadow
 #endif
 #ifndef YRT_EXP_SHADOW_LDS
 #define YRT_EXP_SHADOW_LDS 0  // experiment knob: dynamic LDS per shadow block (occupancy cap)
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
 // WIDE: the 4-wide any-hit walk (timed kernels on scenes whose wide stack fits);
 // otherwise the tracer's binary walk (and always for the instrumented COUNT pass)
 template <bool COUNT, bool PACKET, typename SE, bool WIDE>
-__global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
+__global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
                                                      unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
