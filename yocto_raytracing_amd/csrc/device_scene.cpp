@@ -112,9 +112,14 @@ struct wide_builder {
         const int me = (int)out.size() / 8;
         out.resize(out.size() + 8, f4{0, 0, 0, 0});
         float v[6][4];
-        int ref[4] = {0, 0, 0, 0}, info[4] = {0, 0, 0, 0};
+        // child words (yrt_device.h wide_*): an inner child is its record's byte offset,
+        // a leaf is leaf bit | count << 28 | first slot; an empty slot is a leaf with no
+        // slots behind an inverted infinite box (no finite or infinite ray passes it; a
+        // NaN ray, which passes every box, finds nothing there)
+        uint32_t word[4] = {wide_leaf, wide_leaf, wide_leaf, wide_leaf};
+        bool inner[4] = {false, false, false, false};
         for (int k = 0; k < 4; k++) {
-            if (k >= (int)slots.size()) {  // empty slot: an inverted box, and info 0
+            if (k >= (int)slots.size()) {
                 for (int a = 0; a < 3; a++) v[a][k] = INFINITY, v[3 + a][k] = -INFINITY;
                 continue;
             }
@@ -122,17 +127,24 @@ struct wide_builder {
             v[0][k] = s.bbox.min.x, v[1][k] = s.bbox.min.y, v[2][k] = s.bbox.min.z;
             v[3][k] = s.bbox.max.x, v[4][k] = s.bbox.max.y, v[5][k] = s.bbox.max.z;
             if (s.isleaf) {
-                ref[k] = (int)(s.start + leaf_base);
-                info[k] = (int)((uint32_t)s.count | leaf_bit);
+                const uint32_t first = s.start + leaf_base;
+                if (first > wide_index_mask || s.count > 7)
+                    throw std::runtime_error("scene too large for the wide any-hit records");
+                word[k] = wide_leaf | ((uint32_t)s.count << wide_count_shift) | first;
             } else {
-                info[k] = 1;
+                inner[k] = true;
             }
         }
         for (int k = 0; k < 4; k++)
-            if (info[k] == 1) ref[k] = emit(t, slots[k], leaf_base, depth + 1);
+            if (inner[k]) {
+                const size_t off = (size_t)emit(t, slots[k], leaf_base, depth + 1) * wide_record_bytes;
+                if (off > wide_index_mask) throw std::runtime_error("scene too large for the wide any-hit records");
+                word[k] = (uint32_t)off;
+            }
         for (int a = 0; a < 6; a++) out[(size_t)me * 8 + a] = {v[a][0], v[a][1], v[a][2], v[a][3]};
-        out[(size_t)me * 8 + 6] = {as_float(ref[0]), as_float(ref[1]), as_float(ref[2]), as_float(ref[3])};
-        out[(size_t)me * 8 + 7] = {as_float(info[0]), as_float(info[1]), as_float(info[2]), as_float(info[3])};
+        out[(size_t)me * 8 + 6] = {as_float((int)word[0]), as_float((int)word[1]), as_float((int)word[2]),
+                                   as_float((int)word[3])};
+        out[(size_t)me * 8 + 7] = {as_float((int)slots.size()), 0, 0, 0};
         return me;
     }
 };
@@ -271,8 +283,14 @@ device_scene* device_scene_create(const scene& scn, int device) {
     wnodes.resize(wnodes.size() + 8, f4{0, 0, 0, 0});
     for (int a = 0; a < 3; a++) wnodes[(size_t)wempty * 8 + a] = {INFINITY, INFINITY, INFINITY, INFINITY};
     for (int a = 3; a < 6; a++) wnodes[(size_t)wempty * 8 + a] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    {
+        const float e = as_float((int)wide_leaf);
+        wnodes[(size_t)wempty * 8 + 6] = {e, e, e, e};
+    }
     for (auto& r : wshape_root)
         if (r < 0) r = wempty;
+    if (wnodes.size() / 8 * wide_record_bytes >= (1u << 30))
+        throw std::runtime_error("scene too large for the wide any-hit records");
     // the wide walk pushes at most three siblings per visit
     ds->wide_ok = 3 * (wtop_depth + wshape_depth) + 2 <= 64;
 
@@ -325,9 +343,9 @@ device_scene* device_scene_create(const scene& scn, int device) {
             throw std::runtime_error("instance " + ist.name + " has no material");
         const frame3f& f = ist.frame;
         tinst.push_back({f.x.x, f.x.y, f.x.z, as_float(ist.shp)});
-        // .w: the shape's wide root | kind << 30 (the any-hit walk's entry)
-        const int wr = wshape_root[ist.shp];
-        tinst.push_back({f.y.x, f.y.y, f.y.z, as_float((int)((uint32_t)wr | ((uint32_t)shapes[ist.shp].y << 30)))});
+        // .w: the shape's wide root (record byte offset) | kind << 30 (the any-hit walk's entry)
+        const uint32_t wr = (uint32_t)wshape_root[ist.shp] * (uint32_t)wide_record_bytes;
+        tinst.push_back({f.y.x, f.y.y, f.y.z, as_float((int)(wr | ((uint32_t)shapes[ist.shp].y << 30)))});
         tinst_id.push_back(ii);
         tinst.push_back({f.z.x, f.z.y, f.z.z, as_float(ist.mat)});
         // .w of the last row: the shape's root node and primitive kind, so a traversal
@@ -434,7 +452,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.tpair = (const f4*)(base + o_tpair);
     v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);
-    v.wtop_root = wtop_root;
+    v.wtop_root = wtop_root * wide_record_bytes;
     v.wide = ds->wide_ok ? 1 : 0;
     v.nlights = (int)lights.size() / 6;
     ds->nlights = v.nlights;

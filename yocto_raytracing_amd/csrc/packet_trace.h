@@ -590,172 +590,6 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     return true;
 }
 
-#ifndef YRT_WIDE_HOIST
-#define YRT_WIDE_HOIST 0  // 1: slab-swap signs hoisted to level changes (A/B: +2 %)
-#endif
-#ifndef YRT_WIDE_SKIP
-#define YRT_WIDE_SKIP 1  // scalar branch around empty slots (A/B: shadow -3 %)
-#endif
-
-// ---- any-hit on the 4-wide collapse (device_scene.cpp wide_builder) ----
-// The same packet discipline (SGPR control, VGPR-lane stack, lane masks), over wide
-// nodes: a visit fetches one 128-byte record and every lane of the mask tests the
-// four child boxes with its own ray; the passing children are pushed (the first one
-// is entered directly). Leaves are the reference's: instance leaves enter their
-// instances in slot order, shape leaves test their primitives. A lane leaves the
-// walk at its first hit. Results equal intersect_any's (see wide_builder for why the
-// skipped inner boxes and the order do not matter); the instrumented (COUNT) kernels
-// use the binary walk instead, so work counts stay the reference's.
-#ifdef YRT_WIDE_STATS  // diagnostic: wave-level step counts of the wide walk
-__device__ unsigned long long g_wide_stats[8];
-#define WSTAT(k) \
-    do {                                                                \
-        if (__lane_id() == 0) atomicAdd(&g_wide_stats[(k)], 1ull); \
-    } while (0)
-#else
-#define WSTAT(k) \
-    do {           \
-    } while (0)
-#endif
-
-__device__ __forceinline__ bool packet_occluded_wide(const dev_scene_view& S, const ray3& wray, bool valid) {
-    const int lane = __lane_id();
-    const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
-    if (!live) return false;
-    const vec3f wo = wray.o, wd = wray.d;
-    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
-    const float tmin = wray.tmin, tmax = wray.tmax;
-    vec3f co = wo, cd = wd, ci = wi;
-    bool sx = ci.x < 0, sy = ci.y < 0, sz = ci.z < 0;  // slab swaps, per ray and level
-    int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
-    unsigned long long done = 0, inst_mask = 0;
-    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
-    // the current item: a wide node (info 1) or a leaf (info = count | leaf_bit)
-    int ref = S.wtop_root;
-    uint32_t info = 1;
-    unsigned long long mask = live;
-    for (;;) {
-        if (!(info & leaf_bit)) {
-            WSTAT(0);
-            float4 r[8];
-            ld_records_at<8>(S.wnodes, (unsigned)(8 * ref), r);
-            const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
-                        lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
-                        hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
-            const int rf[4] = {ibits(r[6].x), ibits(r[6].y), ibits(r[6].z), ibits(r[6].w)};
-            const int in[4] = {ibits(r[7].x), ibits(r[7].y), ibits(r[7].z), ibits(r[7].w)};
-            unsigned long long m[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-#if YRT_WIDE_HOIST
-#define WIDE_BOX(k) box_hit6s(co, ci, sx, sy, sz, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])
-#else
-#define WIDE_BOX(k) box_hit6(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k], tn)
-#endif
-                float tn;
-#if YRT_WIDE_SKIP
-                m[k] = 0;
-                // empty slots (info 0) are skipped on a scalar branch
-                if (uniform(in[k]) != 0) m[k] = ballot(WIDE_BOX(k)) & mask;
-#else
-                m[k] = ballot(in[k] != 0 && WIDE_BOX(k)) & mask;
-#endif
-#undef WIDE_BOX
-            }
-            int first = -1;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!m[k]) continue;
-                if (first < 0) {
-                    first = k;
-                    continue;
-                }
-                const bool at = lane_now() == sp;
-                stk_ref = at ? rf[k] : stk_ref;
-                stk_info = at ? in[k] : stk_info;
-                stk_mlo = at ? (int)(uint32_t)m[k] : stk_mlo;
-                stk_mhi = at ? (int)(uint32_t)(m[k] >> 32) : stk_mhi;
-                sp++;
-            }
-            if (first >= 0) {
-                const int rsel = first == 0 ? rf[0] : first == 1 ? rf[1] : first == 2 ? rf[2] : rf[3];
-                const int isel = first == 0 ? in[0] : first == 1 ? in[1] : first == 2 ? in[2] : in[3];
-                ref = uniform(rsel);
-                info = (uint32_t)uniform(isel);
-                mask = m[first];
-                continue;
-            }
-        } else if (level == 0) {
-            WSTAT(1);
-            inst_next = ref;
-            inst_end = ref + (int)(info & 0xffffu);
-            inst_mask = mask;
-            level = 1;
-            base = sp;
-        } else {
-            WSTAT(2);
-            const bool inl = (mask >> lane) & 1;
-            int leaf_hit = 0;
-            const int count = (int)(info & 0xffffu);
-            for (int i = ref; i < ref + count; i++) {
-                float4 pv[3];
-                ld_records<3>(S.sprims + 3 * i, pv);
-                float t;
-                bool h;
-                if (kind == kind_triangles) {
-                    float w1, w2;
-                    h = tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2);
-                } else {
-                    vec4f ew;
-                    const ray3 lr = {co, cd, tmin, tmax};
-                    h = kind == kind_lines ? line_hit(lr, xyz(pv[0]), xyz(pv[1]), pv[1].w, pv[2].x, t, ew)
-                                           : point_hit(lr, xyz(pv[0]), pv[1].x, t, ew);
-                }
-                leaf_hit |= (h && inl) ? 1 : 0;
-            }
-            done |= ballot(leaf_hit != 0);
-            if (!(live & ~done)) return (done >> lane) & 1;
-        }
-        // ---- next: the next instance of the current leaf, or pop ----
-        for (;;) {
-            if (level == 1 && sp == base) {
-                if (inst_next < inst_end) {
-                    WSTAT(3);
-                    const int k = inst_next++;
-                    float4 fr[4];
-                    ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
-                    const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
-                    co = transform_point_inverse(f, wo);
-                    cd = transform_direction_inverse(f, wd);
-                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
-                    sx = ci.x < 0, sy = ci.y < 0, sz = ci.z < 0;
-                    const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
-                    ref = (int)(rk & 0x3fffffffu);
-                    kind = (int)(rk >> 30);
-                    info = 1;
-                    mask = inst_mask & ~done;
-                    if (mask) break;
-                    continue;
-                }
-                level = 0;
-                co = wo;
-                cd = wd;
-                ci = wi;
-                sx = ci.x < 0, sy = ci.y < 0, sz = ci.z < 0;
-            }
-            if (sp == 0) return (done >> lane) & 1;
-            WSTAT(4);
-            sp--;
-            ref = __builtin_amdgcn_readlane(stk_ref, sp);
-            info = (uint32_t)__builtin_amdgcn_readlane(stk_info, sp);
-            const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp);
-            const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp);
-            mask = ((unsigned long long)mhi << 32 | mlo) & ~done;
-            if (mask) break;
-        }
-    }
-}
-
 #ifndef YRT_WIDE_OCTANT
 #define YRT_WIDE_OCTANT 1  // wave-uniform slab signs: near/far planes picked at compile time
 #endif
@@ -792,58 +626,73 @@ __device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes)
     return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
 }
 
-// one descent of the 4-wide any-hit walk: wide nodes from `ref` until a leaf is the
-// current item (mask != 0) or no child passes (mask = 0); the passing children after
-// the first are pushed (v_writelane into lane sp of the stack VGPRs)
+#ifndef YRT_WIDE_SKIP
+#define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
+#endif
+
+// one descent of the 4-wide any-hit walk: from the wide node `cur` (a child word,
+// yrt_device.h) through wide nodes until the current item is a leaf (mask != 0) or no
+// child passes (mask = 0). Children are visited in slot order: the first passing one
+// becomes current, the other passing ones are pushed last-to-first (three v_writelane
+// each: word, mask halves), so they pop in slot order.
 template <int OCT>
 __device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, vec3f ci, float tmin, float tmax,
-                                             int& ref, uint32_t& info, unsigned long long& mask, int& sp,
-                                             int& stk_ref, int& stk_info, int& stk_mlo, int& stk_mhi) {
-        while (!(info & leaf_bit)) {
-            float4 r[8];
-            ld_records_at<8>(S.wnodes, (unsigned)(8 * ref), r);
-            const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
-                        lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
-                        hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
-            const int rf[4] = {uniform(ibits(r[6].x)), uniform(ibits(r[6].y)), uniform(ibits(r[6].z)),
-                               uniform(ibits(r[6].w))};
-            const int in[4] = {uniform(ibits(r[7].x)), uniform(ibits(r[7].y)), uniform(ibits(r[7].z)),
-                               uniform(ibits(r[7].w))};
-            unsigned long long m[4];
+                                             uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
+                                             int& stk_mlo, int& stk_mhi) {
+    const f4* wbase = sgpr_ptr(S.wnodes);
+    for (;;) {
+        float4 r[8];
+        {
+            sgpr16 a, b;
+            asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(a), "=&s"(b)
+                         : "s"(wbase), "s"(cur));
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                m[k] = 0;
-                // empty slots (info 0) are skipped on a scalar branch
-                if (in[k] != 0) m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
-            }
-            int first = -1;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!m[k]) continue;
-                if (first < 0) {
-                    first = k;
-                    continue;
-                }
-                stk_ref = writelane(stk_ref, rf[k], sp);
-                stk_info = writelane(stk_info, in[k], sp);
-                stk_mlo = writelane(stk_mlo, (int)(uint32_t)m[k], sp);
-                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m[k] >> 32), sp);
-                sp++;
-            }
-            if (first < 0) {
-                mask = 0;
-                break;
-            }
-            ref = first == 0 ? rf[0] : first == 1 ? rf[1] : first == 2 ? rf[2] : rf[3];
-            info = (uint32_t)(first == 0 ? in[0] : first == 1 ? in[1] : first == 2 ? in[2] : in[3]);
-            mask = first == 0 ? m[0] : first == 1 ? m[1] : first == 2 ? m[2] : m[3];
+            for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
         }
+        const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
+                    lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
+                    hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
+        const uint32_t w[4] = {(uint32_t)uniform(ibits(r[6].x)), (uint32_t)uniform(ibits(r[6].y)),
+                               (uint32_t)uniform(ibits(r[6].z)), (uint32_t)uniform(ibits(r[6].w))};
+        const int nslots = uniform(ibits(r[7].x));
+        unsigned long long m[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!YRT_WIDE_SKIP || k < 2 || k < nslots)  // every wide node has >= 2 slots but a leaf root's 1
+                m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
+            else
+                m[k] = 0;
+        }
+        unsigned long long cm = 0;
+        uint32_t cw = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; k--) {
+            if (m[k]) {
+                if (cm) {
+                    stk_word = writelane(stk_word, (int)cw, sp);
+                    stk_mlo = writelane(stk_mlo, (int)(uint32_t)cm, sp);
+                    stk_mhi = writelane(stk_mhi, (int)(uint32_t)(cm >> 32), sp);
+                    sp++;
+                }
+                cm = m[k];
+                cw = w[k];
+            }
+        }
+        mask = cm;
+        cur = cw;
+        if (!cm || (cw & wide_leaf)) return;
+    }
 }
 
 // ---- any hit on the 4-wide collapse, laid out for the scalar unit ----
-// packet_occluded_wide's walk (same wide nodes, same push order, same leaves) with
-// packet_first's structure: a single-exit descent loop over wide nodes, the leaf,
-// then the pop loop; pushes are v_writelane of the SGPR values into lane sp.
+// intersect_any (scene.cpp:489) over the 4-wide collapse of the reference BVH
+// (device_scene.cpp wide_builder): the same packet discipline as packet_first (SGPR
+// control, lane masks, a stack in VGPR lanes) over wide nodes. Results equal
+// intersect_any's: every box of the collapse is one the reference tests, a box test is
+// monotone in the box (NaN slabs included), so every leaf reached is one the reference
+// reaches, and the any-hit answer does not depend on the order. The instrumented
+// (COUNT) kernels use the binary walk instead, so work counts stay the reference's.
 __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid) {
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
@@ -852,48 +701,52 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
     const float tmin = wray.tmin, tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = wi;
-    int stk_ref = 0, stk_info = 0, stk_mlo = 0, stk_mhi = 0;
+    int stk_word = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
-    // the current item: a wide node (info 1) or a leaf (info = count | leaf_bit)
-    int ref = S.wtop_root;
-    uint32_t info = 1;
+    // the current item: a child word (a wide node's byte offset, or a leaf)
+    uint32_t cur = (uint32_t)S.wtop_root;
     unsigned long long mask = live;
     // the octant of the current level's rays when the whole wave shares it (8: mixed)
     const int woct = YRT_WIDE_OCTANT ? wave_octant(wi, live) : 8;
     int oct = woct;
     for (;;) {
         // ---- descent through wide nodes until a leaf or no passing child ----
+        if (!(cur & wide_leaf)) {
+            DBG_CHECK(cur < (uint32_t)S.nwnodes * wide_record_bytes && sp >= 0 && sp < 61, 4, (int)cur, sp, level,
+                      base, 0);
 #if YRT_WIDE_OCTANT
-        switch (oct) {
-            case 0: wide_descend<0>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 1: wide_descend<1>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 2: wide_descend<2>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 3: wide_descend<3>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 4: wide_descend<4>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 5: wide_descend<5>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 6: wide_descend<6>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            case 7: wide_descend<7>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-            default: wide_descend<8>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi); break;
-        }
+            switch (oct) {
+                case 0: wide_descend<0>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 1: wide_descend<1>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 2: wide_descend<2>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 3: wide_descend<3>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 4: wide_descend<4>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 5: wide_descend<5>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 6: wide_descend<6>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 7: wide_descend<7>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                default: wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+            }
 #else
-        wide_descend<8>(S, co, ci, tmin, tmax, ref, info, mask, sp, stk_ref, stk_info, stk_mlo, stk_mhi);
+            wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi);
 #endif
+        }
         // ---- the leaf reached, if any ----
         if (mask) {
+            const int first = (int)(cur & wide_index_mask);
+            const int count = (int)((cur >> wide_count_shift) & 7u);
             if (level == 0) {
-                inst_next = ref;
-                inst_end = ref + (int)(info & 0xffffu);
+                inst_next = first;
+                inst_end = first + count;
                 inst_mask = mask;
                 level = 1;
                 base = sp;
             } else {
+                DBG_CHECK(first >= 0 && first + count <= S.nsprims, 5, first, count, level, kind, sp);
                 const bool inl = (mask & me) != 0;
                 int leaf_hit = 0;
-                const int count = (int)(info & 0xffffu);
-                DBG_CHECK(ref >= 0 && ref + count <= S.nsprims, 5, ref, count, level, kind, sp);
                 if (kind == kind_triangles) {
-                    for (int i = ref; i < ref + count; i++) {
+                    for (int i = first; i < first + count; i++) {
                         float4 pv[3];
                         ld_records<3>(S.sprims + 3 * i, pv);
                         float t, w1, w2;
@@ -901,7 +754,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                         leaf_hit |= (h && inl) ? 1 : 0;
                     }
                 } else {
-                    for (int i = ref; i < ref + count; i++) {
+                    for (int i = first; i < first + count; i++) {
                         float4 pv[3];
                         ld_records<3>(S.sprims + 3 * i, pv);
                         float t;
@@ -931,9 +784,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     cd = transform_direction_inverse(f, wd);
                     ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
-                    ref = (int)(rk & 0x3fffffffu);
+                    cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
-                    info = 1;
                     mask = inst_mask & ~done;
                     if (YRT_WIDE_OCTANT) oct = wave_octant(ci, live & ~done);
                     if (mask) break;
@@ -950,8 +802,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 break;
             }
             sp--;
-            ref = __builtin_amdgcn_readlane(stk_ref, sp);
-            info = (uint32_t)__builtin_amdgcn_readlane(stk_info, sp);
+            cur = (uint32_t)__builtin_amdgcn_readlane(stk_word, sp);
             mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
                     (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
                    ~done;

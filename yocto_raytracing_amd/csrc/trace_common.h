@@ -61,21 +61,6 @@ __device__ __forceinline__ bool box_hit6(vec3f o, vec3f invd, float tmin_r, floa
     return tmin <= tmax;
 }
 
-// the same test with the per-axis sign of invd precomputed (sx = invd.x < 0, ...): a
-// walk hoists the three compares to where its ray changes
-__device__ __forceinline__ bool box_hit6s(vec3f o, vec3f invd, bool sx, bool sy, bool sz, float tmin_r, float tmax_r,
-                                          float lx, float ly, float lz, float hx, float hy, float hz) {
-    float t0x = (lx - o.x) * invd.x, t0y = (ly - o.y) * invd.y, t0z = (lz - o.z) * invd.z;
-    float t1x = (hx - o.x) * invd.x, t1y = (hy - o.y) * invd.y, t1z = (hz - o.z) * invd.z;
-    const float nx = sx ? t1x : t0x, fx = sx ? t0x : t1x;
-    const float ny = sy ? t1y : t0y, fy = sy ? t0y : t1y;
-    const float nz = sz ? t1z : t0z, fz = sz ? t0z : t1z;
-    float tmin = fmaxf(fmaxf(fmaxf(nx, ny), nz), tmin_r);
-    float tmax = fminf(fminf(fminf(fx, fy), fz), tmax_r);
-    tmax *= 1.00000024f;
-    return tmin <= tmax;
-}
-
 __device__ __forceinline__ bool box_hit(vec3f o, vec3f invd, float tmin_r, float tmax_r, float4 lo, float4 hi,
                                         float& tnear) {
     return box_hit6(o, invd, tmin_r, tmax_r, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, tnear);

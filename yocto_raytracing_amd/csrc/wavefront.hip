@@ -293,11 +293,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene
         hit_record hr;
         bool occ;
         if constexpr (WIDE)
-#if YRT_PF2
             occ = packet_occluded_wide2(S, sr, valid);
-#else
-            occ = packet_occluded_wide(S, sr, valid);
-#endif
         else
             occ = T.trace(S, sr, valid, hr, wc);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
@@ -664,14 +660,3 @@ extern "C" int yrt_debug_bounds(unsigned* out8, int reset) {
 }
 #endif
 
-#ifdef YRT_WIDE_STATS
-extern "C" int yrt_debug_wide_stats(unsigned long long* out8, int reset) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(yrt::g_wide_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    if (reset) {
-        unsigned long long z[8] = {};
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_wide_stats), z, sizeof z);
-    }
-    return 0;
-}
-#endif

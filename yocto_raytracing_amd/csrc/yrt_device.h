@@ -42,6 +42,16 @@ enum shape_kind : int { kind_triangles = 0, kind_lines = 1, kind_points = 2, kin
 enum mat_flags : int { mat_reflective = 1 };
 
 constexpr uint32_t leaf_bit = 0x80000000u;
+
+// 4-wide any-hit records (device_scene.cpp wide_builder): 128 bytes per wide node --
+// six f4 rows of child bounds {lo.x[4]}, {lo.y[4]}, {lo.z[4]}, {hi.x[4]}, {hi.y[4]},
+// {hi.z[4]}, one f4 of child words, one f4 {slot count, -, -, -}. A child word is the
+// child record's byte offset (inner: usable as the load's SGPR offset as is), or
+// wide_leaf | count << wide_count_shift | first slot (a leaf of the reference BVH).
+constexpr uint32_t wide_leaf = 0x80000000u;
+constexpr int wide_count_shift = 28;
+constexpr uint32_t wide_index_mask = 0x0fffffffu;
+constexpr int wide_record_bytes = 128;
 #ifndef YRT_SPINE
 #define YRT_SPINE 2
 #endif
