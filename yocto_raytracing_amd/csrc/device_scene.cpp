@@ -316,12 +316,20 @@ device_scene* device_scene_create(const scene& scn, int device) {
                     out.push_back({0, 0, 0, 0});
                     continue;
                 }
-                const f4 lo = nodes[2 * y], hi = nodes[2 * y + 1];
-                out.push_back(lo);
-                out.push_back(hi);
+                f4 lo = nodes[2 * y];
+                const f4 hi = nodes[2 * y + 1];
                 uint32_t cl, start;
                 memcpy(&cl, &hi.w, 4);
                 memcpy(&start, &lo.w, 4);
+                if (!(cl & leaf_bit)) {
+                    // an inner node's child: the byte offset of its spine record (from the
+                    // level's first record), the walks' load offset as is
+                    const uint64_t off = (uint64_t)start * spine_record_bytes;
+                    if (off >= (1ull << 31)) throw std::runtime_error("scene too large for the spine records");
+                    lo.w = as_float((int)off);
+                }
+                out.push_back(lo);
+                out.push_back(hi);
                 if (cl & leaf_bit)
                     live = false;
                 else

@@ -279,12 +279,13 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
             if (COUNT && (mj & me)) wc.box++;
             const unsigned long long pm = ballot(pass[j]) & mj;
             if (!pm) break;
-            const int start = uniform(ibits(rec[2 * j].w));
+            const int sw = uniform(ibits(rec[2 * j].w));
             const uint32_t cl = (uint32_t)uniform((int)ubits(rec[2 * j + 1].w));
             if (cl & leaf_bit) {
-                lstart = start, lcl = cl, lmask = pm;
+                lstart = sw, lcl = cl, lmask = pm;
                 break;
             }
+            const int start = sw / spine_record_bytes;  // inner: a record byte offset
             // push start (slot sp of the stack VGPRs := {start, pm}); the reference pops
             // start+1 next and tests it: that is spine node j+1
             const bool at = lane_now() == sp;
@@ -415,6 +416,99 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 #define DBG_CHECK(cond, code, a, b, c, d, e)
 #endif
 
+#ifndef YRT_WIDE_OCTANT
+#define YRT_WIDE_OCTANT 1  // wave-uniform slab signs: near/far planes picked at compile time
+#endif
+
+// intersect_check_bbox (scene.cpp:371-382) with the per-axis swap decided at compile
+// time: OCT bit a set = this lane's invd component a is < 0 (the reference's swap
+// condition). The same two products per axis are computed -- (lo - o) * invd and
+// (hi - o) * invd -- and each lands where the reference's swap puts it, so the values
+// are bit-identical; OCT 8 is the run-time select of box_hit6.
+template <int OCT>
+__device__ __forceinline__ bool box_oct(vec3f o, vec3f invd, float tmin_r, float tmax_r, float lx, float ly, float lz,
+                                        float hx, float hy, float hz) {
+    if constexpr (OCT == 8) {
+        float tn;
+        return box_hit6(o, invd, tmin_r, tmax_r, lx, ly, lz, hx, hy, hz, tn);
+    } else {
+        const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
+        const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
+        const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
+        const float t0x = (nx - o.x) * invd.x, t0y = (ny - o.y) * invd.y, t0z = (nz - o.z) * invd.z;
+        const float t1x = (fx - o.x) * invd.x, t1y = (fy - o.y) * invd.y, t1z = (fz - o.z) * invd.z;
+        float tmin = fmaxf(fmaxf(fmaxf(t0x, t0y), t0z), tmin_r);
+        float tmax = fminf(fminf(fminf(t1x, t1y), t1z), tmax_r);
+        tmax *= 1.00000024f;
+        return tmin <= tmax;
+    }
+}
+
+// the octant shared by every lane of `lanes` (bit a: invd component a < 0), or 8
+__device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes) {
+    const unsigned long long nx = ballot(invd.x < 0) & lanes, ny = ballot(invd.y < 0) & lanes,
+                             nz = ballot(invd.z < 0) & lanes;
+    if ((nx && nx != lanes) || (ny && ny != lanes) || (nz && nz != lanes)) return 8;
+    return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
+}
+
+#ifndef YRT_FIRST_OCTANT
+#define YRT_FIRST_OCTANT 1  // closest hit: octant-specialised slab tests (see box_oct)
+#endif
+
+// one descent of the closest-hit walk from the spine record at byte offset `node` of
+// pbase: returns with mask = 0 when no lane passes, or with a leaf reached (mask: its
+// lanes, node: its first slot, cl: count | leaf_bit). Per spine node: one ballot &
+// mask, one leaf test, one push (v_writelane of the record offset and lane mask).
+template <int OCT, bool COUNT>
+__device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
+                                              unsigned long long me, int& node, unsigned long long& mask, int& sp,
+                                              int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
+                                              work_counts& wc) {
+    for (;;) {
+        float4 rec[4];
+        {
+            sgpr16 a;
+            asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
+                         : "=s"(a)
+                         : "s"(sgpr_ptr(pbase)), "s"(uniform(node)));
+            rec[0] = rec_of(a, 0), rec[1] = rec_of(a, 1), rec[2] = rec_of(a, 2), rec[3] = rec_of(a, 3);
+        }
+        const bool p0 = box_oct<OCT>(co, ci, tmin, tmax, rec[0].x, rec[0].y, rec[0].z, rec[1].x, rec[1].y, rec[1].z);
+        const bool p1 = box_oct<OCT>(co, ci, tmin, tmax, rec[2].x, rec[2].y, rec[2].z, rec[3].x, rec[3].y, rec[3].z);
+        if (COUNT && (me & 1)) wc.wnode++;
+        if (COUNT && (mask & me)) wc.box++;
+        const unsigned long long pm0 = ballot(p0) & mask;
+        mask = pm0;
+        if (!pm0) return;
+        const int s0 = uniform(ibits(rec[0].w));
+        const uint32_t c0 = (uint32_t)uniform(ibits(rec[1].w));
+        if (c0 & leaf_bit) {
+            node = s0, cl = c0;
+            return;
+        }
+        stk_node = writelane(stk_node, s0, sp);
+        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
+        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
+        sp++;
+        if (COUNT && (pm0 & me)) wc.box++;
+        const unsigned long long pm1 = ballot(p1) & pm0;
+        mask = pm1;
+        if (!pm1) return;
+        const int s1 = uniform(ibits(rec[2].w));
+        const uint32_t c1 = (uint32_t)uniform(ibits(rec[3].w));
+        if (c1 & leaf_bit) {
+            node = s1, cl = c1;
+            return;
+        }
+        stk_node = writelane(stk_node, s1, sp);
+        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
+        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
+        sp++;
+        node = s1 + spine_record_bytes;
+    }
+}
+
 // ---- closest hit, laid out for the scalar unit ----
 // The same walk as packet_trace<false> (same node tests, in the same order, with the
 // same tmax per lane), with the control flow written as explicit states joined by
@@ -440,51 +534,36 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0, mask = live;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
-    int node = 0;
+    int node = 0;  // byte offset of the current spine record from pbase
     const f4* pbase = S.tpair;
+    const int woct = YRT_FIRST_OCTANT ? wave_octant(ci, live) : 8;
+    int oct = woct;
     for (;;) {
         // ---- descent: one spine record per step, until a leaf or no passing lane ----
-        unsigned long long lmask = 0;
-        int lstart = 0, lcount = 0;
-        for (;;) {
-            DBG_CHECK(node >= 0 && sp >= 0 && sp < 63 &&
-                          (level == 0 ? node < S.ntnodes : (int)((pbase - S.spair) / 4) + node < S.nsnodes),
-                      1, node, sp, level, (int)((pbase - S.spair) / 4), base);
-            float4 rec[4];
-            ld_records_at<4>(pbase, (unsigned)(4 * node), rec);
-            const bool p0 = box_hit(co, ci, tmin, tmax, rec[0], rec[1]);
-            const bool p1 = box_hit(co, ci, tmin, tmax, rec[2], rec[3]);
-            if (COUNT && (me & 1)) wc.wnode++;
-            if (COUNT && (mask & me)) wc.box++;
-            const unsigned long long pm0 = ballot(p0) & mask;
-            if (!pm0) break;
-            const int s0 = uniform(ibits(rec[0].w));
-            const uint32_t c0 = (uint32_t)uniform(ibits(rec[1].w));
-            if (c0 & leaf_bit) {
-                lstart = s0, lcount = (int)(c0 & 0xffffu), lmask = pm0;
-                break;
-            }
-            // push start; the reference pops start+1 next and tests it: spine node 1
-            stk_node = writelane(stk_node, s0, sp);
-            stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
-            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
-            sp++;
-            if (COUNT && (pm0 & me)) wc.box++;
-            const unsigned long long pm1 = ballot(p1) & pm0;
-            if (!pm1) break;
-            const int s1 = uniform(ibits(rec[2].w));
-            const uint32_t c1 = (uint32_t)uniform(ibits(rec[3].w));
-            if (c1 & leaf_bit) {
-                lstart = s1, lcount = (int)(c1 & 0xffffu), lmask = pm1;
-                break;
-            }
-            stk_node = writelane(stk_node, s1, sp);
-            stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
-            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
-            sp++;
-            node = s1 + 1;
-            mask = pm1;
+        DBG_CHECK(node >= 0 && (node % spine_record_bytes) == 0 && sp >= 0 && sp < 63 &&
+                      (level == 0 ? node / spine_record_bytes < S.ntnodes
+                                  : (int)((pbase - S.spair) / 4) + node / spine_record_bytes < S.nsnodes),
+                  1, node, sp, level, (int)((pbase - S.spair) / 4), base);
+        uint32_t lcl = 0;
+#define YRT_FD(o) first_descend<o, COUNT>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc)
+#if YRT_FIRST_OCTANT
+        switch (oct) {
+            case 0: YRT_FD(0); break;
+            case 1: YRT_FD(1); break;
+            case 2: YRT_FD(2); break;
+            case 3: YRT_FD(3); break;
+            case 4: YRT_FD(4); break;
+            case 5: YRT_FD(5); break;
+            case 6: YRT_FD(6); break;
+            case 7: YRT_FD(7); break;
+            default: YRT_FD(8); break;
         }
+#else
+        YRT_FD(8);
+#endif
+#undef YRT_FD
+        const unsigned long long lmask = mask;
+        const int lstart = node, lcount = (int)(lcl & 0xffffu);
         // ---- the leaf reached, if any ----
         if (lmask) {
             if (level == 0) {
@@ -560,6 +639,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     mask = inst_mask & ~done;
                     if (COUNT && (mask & me)) wc.inst++;
                     node = 0;  // the shape root, tested like any popped node
+                    if (YRT_FIRST_OCTANT) oct = wave_octant(ci, live & ~done);
                     if (mask) break;
                     continue;
                 }
@@ -568,6 +648,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 co = wo;
                 cd = wd;
                 ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+                oct = woct;
             }
             if (sp == 0) {
                 finished = true;
@@ -590,42 +671,6 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     return true;
 }
 
-#ifndef YRT_WIDE_OCTANT
-#define YRT_WIDE_OCTANT 1  // wave-uniform slab signs: near/far planes picked at compile time
-#endif
-
-// intersect_check_bbox (scene.cpp:371-382) with the per-axis swap decided at compile
-// time: OCT bit a set = this lane's invd component a is < 0 (the reference's swap
-// condition). The same two products per axis are computed -- (lo - o) * invd and
-// (hi - o) * invd -- and each lands where the reference's swap puts it, so the values
-// are bit-identical; OCT 8 is the run-time select of box_hit6.
-template <int OCT>
-__device__ __forceinline__ bool box_oct(vec3f o, vec3f invd, float tmin_r, float tmax_r, float lx, float ly, float lz,
-                                        float hx, float hy, float hz) {
-    if constexpr (OCT == 8) {
-        float tn;
-        return box_hit6(o, invd, tmin_r, tmax_r, lx, ly, lz, hx, hy, hz, tn);
-    } else {
-        const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
-        const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
-        const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
-        const float t0x = (nx - o.x) * invd.x, t0y = (ny - o.y) * invd.y, t0z = (nz - o.z) * invd.z;
-        const float t1x = (fx - o.x) * invd.x, t1y = (fy - o.y) * invd.y, t1z = (fz - o.z) * invd.z;
-        float tmin = fmaxf(fmaxf(fmaxf(t0x, t0y), t0z), tmin_r);
-        float tmax = fminf(fminf(fminf(t1x, t1y), t1z), tmax_r);
-        tmax *= 1.00000024f;
-        return tmin <= tmax;
-    }
-}
-
-// the octant shared by every lane of `lanes` (bit a: invd component a < 0), or 8
-__device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes) {
-    const unsigned long long nx = ballot(invd.x < 0) & lanes, ny = ballot(invd.y < 0) & lanes,
-                             nz = ballot(invd.z < 0) & lanes;
-    if ((nx && nx != lanes) || (ny && ny != lanes) || (nz && nz != lanes)) return 8;
-    return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
-}
-
 #ifndef YRT_WIDE_SKIP
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
@@ -646,7 +691,7 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, 
             sgpr16 a, b;
             asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
                          : "=&s"(a), "=&s"(b)
-                         : "s"(wbase), "s"(cur));
+                         : "s"(wbase), "s"(uniform((int)cur)));
 #pragma unroll
             for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
         }

@@ -56,6 +56,9 @@ constexpr int wide_record_bytes = 128;
 #define YRT_SPINE 2
 #endif
 constexpr int spine_len = YRT_SPINE;  // nodes per closest-hit walk record (2..4)
+// spine records (tpair/spair): spine_len x {lo, hi} f4 pairs; an inner node's lo.w is
+// the byte offset of its child start's record (child start+1's is the next record)
+constexpr int spine_record_bytes = 32 * spine_len;
 
 struct dev_scene_view {
     const f4* tnodes;
