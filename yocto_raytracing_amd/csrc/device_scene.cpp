@@ -101,7 +101,13 @@ struct wide_builder {
             const vec3f d = b.max - b.min;
             return d.x * d.y + d.y * d.z + d.z * d.x;
         };
-        if (YRT_WIDE_SORT == 2)  // leaves first, then smallest
+        if (YRT_WIDE_SORT == 3)  // lowest first (experiment: up-going shadow rays)
+            std::stable_sort(slots.begin(), slots.end(),
+                             [&](int a, int b) { return t.nodes[a].bbox.min.y < t.nodes[b].bbox.min.y; });
+        else if (YRT_WIDE_SORT == 4)  // highest first
+            std::stable_sort(slots.begin(), slots.end(),
+                             [&](int a, int b) { return t.nodes[a].bbox.max.y > t.nodes[b].bbox.max.y; });
+        else if (YRT_WIDE_SORT == 2)  // leaves first, then smallest
             std::stable_sort(slots.begin(), slots.end(), [&](int a, int b) {
                 const bool la = t.nodes[a].isleaf, lb = t.nodes[b].isleaf;
                 return la != lb ? la : area(a) < area(b);
