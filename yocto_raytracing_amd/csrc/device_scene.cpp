@@ -69,6 +69,114 @@ struct arena_builder {
 // Record (8 x f4, 128 bytes): lo.x[4] lo.y[4] lo.z[4] hi.x[4] hi.y[4] hi.z[4], then
 // per slot the reference (wide node index, or first leaf slot + `leaf_base`) and the
 // info (0 empty slot, 1 inner, count | leaf_bit for a leaf).
+// A binary tree over the LEAVES of a reference BVH, built with binned SAH, for the
+// any-hit walk only. Its leaves are the reference's leaves (same boxes, same primitive
+// slots); its inner boxes are unions of leaf boxes, so each one contains every leaf
+// below it. A box test is monotone in the box (NaN slabs included), so a leaf's own box
+// passing implies every ancestor's passes -- in this tree and in the reference's alike:
+// the set of leaves a ray reaches is the same in both trees, and so is the any-hit
+// answer, which does not depend on the order. What changes is how many inner boxes the
+// walk tests to get there. (The closest-hit walk keeps the reference tree: its tie-break
+// depends on the order.)
+struct sah_builder {
+    struct item {
+        bbox3f box;
+        vec3f c;
+        int leaf;  // reference node index
+    };
+    const bvh_tree& ref;
+    std::vector<item> items;
+    bvh_tree out;
+    int max_depth = 0;
+
+    static float area(const bbox3f& b) {
+        const vec3f d = b.max - b.min;
+        return d.x * d.y + d.y * d.z + d.z * d.x;
+    }
+
+    explicit sah_builder(const bvh_tree& t) : ref(t) {
+        for (size_t i = 0; i < t.nodes.size(); i++)
+            if (t.nodes[i].isleaf) {
+                const bbox3f& b = t.nodes[i].bbox;
+                items.push_back({b, (b.min + b.max) * 0.5f, (int)i});
+            }
+        out.leaf_prims = t.leaf_prims;
+        if (items.empty()) return;
+        out.nodes.reserve(2 * items.size());
+        out.nodes.push_back({});
+        build(0, 0, (int)items.size(), 1);
+    }
+
+    void build(int x, int b, int e, int depth) {
+        max_depth = std::max(max_depth, depth);
+        bbox3f box = invalid_bbox3f, cb = invalid_bbox3f;
+        for (int i = b; i < e; i++) box = expand_bbox(box, items[i].box), cb = expand_bbox(cb, items[i].c);
+        if (e - b == 1) {
+            out.nodes[x] = ref.nodes[items[b].leaf];
+            return;
+        }
+        // binned SAH over the leaf centroids, every axis
+        constexpr int NB = 32;
+        float best = INFINITY;
+        int best_axis = -1, best_bin = 0;
+        for (int a = 0; a < 3; a++) {
+            const float lo = (&cb.min.x)[a], hi = (&cb.max.x)[a];
+            if (!(hi > lo)) continue;
+            bbox3f bb[NB];
+            int bn[NB] = {};
+            for (auto& q : bb) q = invalid_bbox3f;
+            for (int i = b; i < e; i++) {
+                int k = (int)((((&items[i].c.x)[a]) - lo) / (hi - lo) * NB);
+                k = std::min(std::max(k, 0), NB - 1);
+                bb[k] = expand_bbox(bb[k], items[i].box);
+                bn[k]++;
+            }
+            float la[NB];
+            int ln[NB];
+            bbox3f acc = invalid_bbox3f;
+            int n = 0;
+            for (int k = 0; k < NB; k++) {
+                acc = expand_bbox(acc, bb[k]);
+                n += bn[k];
+                la[k] = n ? area(acc) : 0.0f, ln[k] = n;
+            }
+            acc = invalid_bbox3f;
+            n = 0;
+            for (int k = NB - 1; k > 0; k--) {
+                acc = expand_bbox(acc, bb[k]);
+                n += bn[k];
+                if (!n || !ln[k - 1]) continue;
+                const float cost = la[k - 1] * (float)ln[k - 1] + area(acc) * (float)n;
+                if (cost < best) best = cost, best_axis = a, best_bin = k;
+            }
+        }
+        int mid;
+        if (best_axis < 0) {  // coincident centroids: split the range in half
+            mid = (b + e) / 2;
+        } else {
+            const float lo = (&cb.min.x)[best_axis], hi = (&cb.max.x)[best_axis];
+            auto it = std::partition(items.begin() + b, items.begin() + e, [&](const item& q) {
+                int k = (int)((((&q.c.x)[best_axis]) - lo) / (hi - lo) * NB);
+                k = std::min(std::max(k, 0), NB - 1);
+                return k < best_bin;
+            });
+            mid = (int)(it - items.begin());
+            if (mid == b || mid == e) mid = (b + e) / 2;
+        }
+        const int c = (int)out.nodes.size();
+        out.nodes.push_back({});
+        out.nodes.push_back({});
+        bvh_node& n = out.nodes[x];
+        n.bbox = box;
+        n.start = (uint32_t)c;
+        n.count = 2;
+        n.isleaf = 0;
+        n.axis = (uint8_t)std::max(best_axis, 0);
+        build(c, b, mid, depth + 1);
+        build(c + 1, mid, e, depth + 1);
+    }
+};
+
 struct wide_builder {
     std::vector<f4>& out;
     int max_depth = 0;
@@ -273,15 +381,25 @@ device_scene* device_scene_create(const scene& scn, int device) {
     }
 
     // ---- 4-wide collapse for the any-hit walk: instance level first, then shapes ----
+    // over the reference trees, or (YRT_WIDE_SAH) over SAH trees of their leaves
+#ifndef YRT_WIDE_SAH
+#define YRT_WIDE_SAH 1
+#endif
+    auto any_tree = [](const bvh_tree& t) {
+        if (!YRT_WIDE_SAH || t.nodes.empty()) return t;
+        sah_builder sb(t);
+        return sb.out;
+    };
     std::vector<f4> wnodes;
     wide_builder wb{wnodes};
-    const int wtop_root = wb.emit(scn.bvh, 0, 0, 1);
+    const int wtop_root = wb.emit(any_tree(scn.bvh), 0, 0, 1);
     const int wtop_depth = wb.max_depth;
     std::vector<int> wshape_root(scn.shapes.size());
     int wshape_depth = 0;
     for (size_t si = 0; si < scn.shapes.size(); si++) {
         wb.max_depth = 0;
-        wshape_root[si] = scn.shapes[si].bvh.nodes.empty() ? -1 : wb.emit(scn.shapes[si].bvh, 0, shape_prim_base[si], 1);
+        wshape_root[si] =
+            scn.shapes[si].bvh.nodes.empty() ? -1 : wb.emit(any_tree(scn.shapes[si].bvh), 0, shape_prim_base[si], 1);
         wshape_depth = std::max(wshape_depth, wb.max_depth);
     }
     // instances of an empty shape enter a wide node with no slots

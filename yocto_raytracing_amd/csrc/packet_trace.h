@@ -211,7 +211,11 @@ __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float t
                                            float& t, float& w1, float& w2) {
     vec3f r = cross(d, e2);
     float den = dot(r, e1);
+#ifdef YRT_EXP_FASTTRI  // timing diagnostic only: approximate reciprocal (results differ)
+    float inv_den = __builtin_amdgcn_rcpf(den);
+#else
     float inv_den = 1.0f / den;
+#endif
     vec3f c = o - v0;
     w1 = dot(r, c) * inv_den;
     vec3f s = cross(c, e1);
@@ -415,6 +419,22 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 #else
 #define DBG_CHECK(cond, code, a, b, c, d, e)
 #endif
+
+// the instance-local direction and its inverse on instance entry (transform_ray_inverse,
+// vmath.h:275-278: the direction renormalized, invd = 1/d as intersect_check_bbox
+// computes it). YRT_EXP_FASTINST is a timing diagnostic only (approximate rcp/rsqrt,
+// results differ): it prices the exact math of an instance entry.
+__device__ __forceinline__ void enter_direction(const frame3f& f, vec3f wd, vec3f& cd, vec3f& ci) {
+#ifdef YRT_EXP_FASTINST
+    const vec3f v = {dot(f.x, wd), dot(f.y, wd), dot(f.z, wd)};
+    const float r = __builtin_amdgcn_rsqf(dot(v, v));
+    cd = {v.x * r, v.y * r, v.z * r};
+    ci = {__builtin_amdgcn_rcpf(cd.x), __builtin_amdgcn_rcpf(cd.y), __builtin_amdgcn_rcpf(cd.z)};
+#else
+    cd = transform_direction_inverse(f, wd);
+    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+#endif
+}
 
 #ifndef YRT_WIDE_OCTANT
 #define YRT_WIDE_OCTANT 1  // wave-uniform slab signs: near/far planes picked at compile time
@@ -630,8 +650,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-                    cd = transform_direction_inverse(f, wd);
-                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    enter_direction(f, wd, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[3].w));
                     pbase = S.spair + 2 * spine_len * (rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
@@ -826,8 +845,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-                    cd = transform_direction_inverse(f, wd);
-                    ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
+                    enter_direction(f, wd, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
