@@ -472,6 +472,11 @@ __device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes)
     return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
 }
 
+#ifndef YRT_WI_LDS
+#define YRT_WI_LDS 1  // closest hit: the world 1/d kept in LDS across instance leaves (A/B: primary -1 %)
+#endif
+constexpr int packet_block = 256;  // threads per block of every kernel that runs packet_first
+
 #ifndef YRT_FIRST_OCTANT
 #define YRT_FIRST_OCTANT 1  // closest hit: octant-specialised slab tests (see box_oct)
 #endif
@@ -549,6 +554,12 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     const float tmin = wray.tmin;
     float tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+#if YRT_WI_LDS
+    // the world inverse direction, parked in LDS for the returns from instance leaves
+    // (three ds_read instead of three IEEE divisions; three VGPRs stay free)
+    __shared__ float wi_lds[3][packet_block];
+    wi_lds[0][threadIdx.x] = ci.x, wi_lds[1][threadIdx.x] = ci.y, wi_lds[2][threadIdx.x] = ci.z;
+#endif
     float hw1 = 0, hw2 = 0;
     int hslot = -1, hei = -1;
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
@@ -666,7 +677,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 pbase = S.tpair;
                 co = wo;
                 cd = wd;
+#if YRT_WI_LDS
+                ci = {wi_lds[0][threadIdx.x], wi_lds[1][threadIdx.x], wi_lds[2][threadIdx.x]};
+#else
                 ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+#endif
                 oct = woct;
             }
             if (sp == 0) {
@@ -745,6 +760,23 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, 
         }
         mask = cm;
         cur = cw;
+#ifdef YRT_EXP_SALU  // sensitivity diagnostic: N extra SALU per wide step (A/B: +8 -> shadow +3.4 %)
+        {
+            int d;
+            asm volatile("s_mov_b32 %0, 0" : "=s"(d));
+#pragma unroll
+            for (int q = 0; q < YRT_EXP_SALU; q++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d) : : "scc");
+            asm volatile("" ::"s"(d));
+        }
+#endif
+#ifdef YRT_EXP_VALU  // sensitivity diagnostic: N extra VALU per wide step (A/B: +8 -> shadow +2.2 %)
+        {
+            float d = co.x;
+#pragma unroll
+            for (int q = 0; q < YRT_EXP_VALU; q++) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
+            asm volatile("" ::"v"(d));
+        }
+#endif
         if (!cm || (cw & wide_leaf)) return;
     }
 }
