@@ -185,13 +185,32 @@ __device__ __forceinline__ tracer<ANY, COUNT, PACKET, SE> make_tracer(traversal_
     return t;
 }
 
+#ifndef YRT_XCD_REMAP
+#define YRT_XCD_REMAP 0  // 1: contiguous tile ranges per XCD (A/B at c4: primary +10 %, shadow +7.5 % -- the
+                         // regions differ in cost, and the slowest XCD sets the launch time)
+#endif
+// Workgroups are dealt round-robin to the 8 XCDs (linear block b runs on XCD b % 8).
+// Remap so that each XCD's blocks take one contiguous range of the grid: neighbouring
+// tiles trace neighbouring rays through the same BVH nodes, so each XCD's L2 (and each
+// CU's scalar cache) sees one region of the image instead of every eighth tile of all
+// of it. A bijection for any grid size.
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
+#if YRT_XCD_REMAP
+    const unsigned x = b % 8u, j = b / 8u, q = n / 8u, r = n % 8u;
+    return x * q + (x < r ? x : r) + j;
+#else
+    (void)n;
+    return b;
+#endif
+}
+
 // ---- level 0: camera rays + closest hit + surface ----
 template <bool COUNT, bool PACKET, typename SE>
 __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A, chunk_args C,
                                                       wf_buffers B, unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
-    const int idx = blockIdx.x * WF_BLOCK + threadIdx.x;
+    const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * WF_BLOCK + threadIdx.x;
     const int nsamp = C.npix * C.spp;
     work_counts wc;
     bool valid = false;
@@ -266,7 +285,11 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
     const int n = level ? B.count[level] : nsamp_level0;
-    const int li = blockIdx.y;
+    // level 0 (one block per 256 samples and light): the remap runs over the whole
+    // (x, light) grid; levels >= 1 are grid-stride and keep their blocks
+    const unsigned lin = level ? blockIdx.x : xcd_block(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int li = level ? (int)blockIdx.y : (int)(lin / gridDim.x);
+    const int bx = level ? (int)blockIdx.x : (int)(lin % gridDim.x);
     const f4* lr = S.lights + 6 * li;
     const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
     const vec3f lp0 = xyz(ld4(lr + 4));
@@ -275,7 +298,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene
     const int stride = gridDim.x * WF_BLOCK;
     const int nround = (n + stride - 1) / stride;
     for (int round = 0; round < nround; round++) {
-        const int idx = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
+        const int idx = round * stride + bx * WF_BLOCK + threadIdx.x;
         bool valid = false;
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
         if (idx < n) {
@@ -357,6 +380,8 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                 }
                 if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, uv, wc);
                 vec3f c = {0.0f, 0.0f, 0.0f};
+                // raytrace.cpp:147 (per light) and :196 (mirror): the same value each time
+                const vec3f v = normalize(ro - p);
                 for (int li = 0; li < S.nlights; li++) {
                     if (B.occl[(size_t)li * B.capacity + idx]) continue;
                     const f4* lr = S.lights + 6 * li;
@@ -365,7 +390,6 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                     vec3f tp = transform_point(lf, lp0 - p);
                     vec3f l = normalize(tp);
                     float r = length(tp);
-                    vec3f v = normalize(ro - p);
                     vec3f h = normalize(v + l);
                     vec3f kd = kd0, ks = ks0;
                     if (kd_txt >= 0) kd = kd * tkd;
@@ -396,7 +420,6 @@ __global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render
                     R = (c + t) + la;
                 } else {
                     spawn = true;
-                    vec3f v = normalize(ro - p);
                     dr = (nrm * 2.0f * dot(nrm, v)) - v;
                     rec_d = c;
                     rec_la = la;
