@@ -39,6 +39,7 @@
 // rejects scenes whose instance + shape BVH depth exceeds traversal_stack_cap).
 #pragma once
 
+#include "fast_div.h"
 #include "trace_common.h"
 
 namespace yrt {
@@ -420,17 +421,46 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 #define DBG_CHECK(cond, code, a, b, c, d, e)
 #endif
 
+#ifndef YRT_FAST_DIV
+#define YRT_FAST_DIV 1
+#endif
+
 // the instance-local direction and its inverse on instance entry (transform_ray_inverse,
 // vmath.h:275-278: the direction renormalized, invd = 1/d as intersect_check_bbox
 // computes it). YRT_EXP_FASTINST is a timing diagnostic only (approximate rcp/rsqrt,
 // results differ): it prices the exact math of an instance entry.
-__device__ __forceinline__ void enter_direction(const frame3f& f, vec3f wd, vec3f& cd, vec3f& ci) {
+//
+// The four reciprocals (normalize's 1/l, vmath.h:118-122, and invd) are exact IEEE
+// divisions in the reference. With YRT_FAST_DIV they are rcp_nr (fast_div.h: v_rcp_f32
+// plus one Newton step, bit-identical to 1.0f / x on every input it admits -- checked on
+// all 2^32 floats) whenever every live lane's l and cd components are in the normal range;
+// otherwise (a zero, subnormal, huge, infinite or NaN value in some lane) the wave takes
+// the division.
+__device__ __forceinline__ void enter_direction(const frame3f& f, vec3f wd, unsigned long long lanes, vec3f& cd,
+                                                vec3f& ci) {
 #ifdef YRT_EXP_FASTINST
     const vec3f v = {dot(f.x, wd), dot(f.y, wd), dot(f.z, wd)};
     const float r = __builtin_amdgcn_rsqf(dot(v, v));
     cd = {v.x * r, v.y * r, v.z * r};
     ci = {__builtin_amdgcn_rcpf(cd.x), __builtin_amdgcn_rcpf(cd.y), __builtin_amdgcn_rcpf(cd.z)};
 #else
+#if YRT_FAST_DIV
+    {
+        const vec3f v = {dot(f.x, wd), dot(f.y, wd), dot(f.z, wd)};
+        const float l = length(v);
+        const float y = rcp_nr(l);
+        const vec3f c = v * y;
+        const float lo = fminf(fminf(l, fabsf(c.x)), fminf(fabsf(c.y), fabsf(c.z)));
+        const float hi = fmaxf(fmaxf(l, fabsf(c.x)), fmaxf(fabsf(c.y), fabsf(c.z)));
+        // l == l: a NaN component makes l NaN (fminf/fmaxf would drop it)
+        const bool fast = (l == l) && lo >= 0x1p-126f && hi < 0x1p126f;
+        if (!(ballot(!fast) & lanes)) {
+            cd = c;
+            ci = {rcp_nr(c.x), rcp_nr(c.y), rcp_nr(c.z)};
+            return;
+        }
+    }
+#endif
     cd = transform_direction_inverse(f, wd);
     ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
 #endif
@@ -661,7 +691,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-                    enter_direction(f, wd, cd, ci);
+                    enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[3].w));
                     pbase = S.spair + 2 * spine_len * (rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
@@ -877,7 +907,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-                    enter_direction(f, wd, cd, ci);
+                    enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
