@@ -502,6 +502,26 @@ __device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes)
     return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
 }
 
+#ifndef YRT_INNER_POP
+#define YRT_INNER_POP 1  // descents pop inside their octant's loop (no re-dispatch per pop)
+#endif
+
+// pop inside a descent: entries above `floor` until one with live lanes (true), or down
+// to the floor (false, mask 0) -- the level boundary is the caller's
+__device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, int& node, unsigned long long& mask,
+                                          int& sp, int stk_node, int stk_mlo, int stk_mhi) {
+    while (sp > floor) {
+        sp--;
+        node = __builtin_amdgcn_readlane(stk_node, sp);
+        mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
+                (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
+               ~done;
+        if (mask) return true;
+    }
+    mask = 0;
+    return false;
+}
+
 #ifndef YRT_WI_LDS
 #define YRT_WI_LDS 1  // closest hit: the world 1/d kept in LDS across instance leaves (A/B: primary -1 %)
 #endif
@@ -519,7 +539,7 @@ template <int OCT, bool COUNT>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
-                                              work_counts& wc) {
+                                              work_counts& wc, int floor, unsigned long long done) {
     for (;;) {
         float4 rec[4];
         {
@@ -535,7 +555,12 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         if (COUNT && (mask & me)) wc.box++;
         const unsigned long long pm0 = ballot(p0) & mask;
         mask = pm0;
-        if (!pm0) return;
+        if (!pm0) {
+#if YRT_INNER_POP
+            if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
+#endif
+            return;
+        }
         const int s0 = uniform(ibits(rec[0].w));
         const uint32_t c0 = (uint32_t)uniform(ibits(rec[1].w));
         if (c0 & leaf_bit) {
@@ -549,7 +574,12 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         if (COUNT && (pm0 & me)) wc.box++;
         const unsigned long long pm1 = ballot(p1) & pm0;
         mask = pm1;
-        if (!pm1) return;
+        if (!pm1) {
+#if YRT_INNER_POP
+            if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
+#endif
+            return;
+        }
         const int s1 = uniform(ibits(rec[2].w));
         const uint32_t c1 = (uint32_t)uniform(ibits(rec[3].w));
         if (c1 & leaf_bit) {
@@ -606,7 +636,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                                   : (int)((pbase - S.spair) / 4) + node / spine_record_bytes < S.nsnodes),
                   1, node, sp, level, (int)((pbase - S.spair) / 4), base);
         uint32_t lcl = 0;
-#define YRT_FD(o) first_descend<o, COUNT>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc)
+        const int floor = level ? base : 0;
+#define YRT_FD(o) \
+    first_descend<o, COUNT>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc, floor, done)
 #if YRT_FIRST_OCTANT
         switch (oct) {
             case 0: YRT_FD(0); break;
@@ -747,7 +779,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 template <int OCT>
 __device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, vec3f ci, float tmin, float tmax,
                                              uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
-                                             int& stk_mlo, int& stk_mhi) {
+                                             int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
     const f4* wbase = sgpr_ptr(S.wnodes);
     for (;;) {
         float4 r[8];
@@ -807,7 +839,21 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, 
             asm volatile("" ::"v"(d));
         }
 #endif
-        if (!cm || (cw & wide_leaf)) return;
+        if (cm) {
+            if (cw & wide_leaf) return;
+            continue;
+        }
+#if YRT_INNER_POP
+        {
+            int n = 0;
+            if (inner_pop(floor, done, n, mask, sp, stk_word, stk_mlo, stk_mhi)) {
+                cur = (uint32_t)n;
+                if (cur & wide_leaf) return;
+                continue;
+            }
+        }
+#endif
+        return;
     }
 }
 
@@ -839,22 +885,23 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     for (;;) {
         // ---- descent through wide nodes until a leaf or no passing child ----
         if (!(cur & wide_leaf)) {
+            const int wfloor = level ? base : 0;
             DBG_CHECK(cur < (uint32_t)S.nwnodes * wide_record_bytes && sp >= 0 && sp < 61, 4, (int)cur, sp, level,
                       base, 0);
 #if YRT_WIDE_OCTANT
             switch (oct) {
-                case 0: wide_descend<0>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 1: wide_descend<1>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 2: wide_descend<2>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 3: wide_descend<3>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 4: wide_descend<4>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 5: wide_descend<5>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 6: wide_descend<6>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                case 7: wide_descend<7>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
-                default: wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi); break;
+                case 0: wide_descend<0>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 1: wide_descend<1>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 2: wide_descend<2>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 3: wide_descend<3>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 4: wide_descend<4>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 5: wide_descend<5>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 6: wide_descend<6>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 7: wide_descend<7>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                default: wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
             }
 #else
-            wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi);
+            wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done);
 #endif
         }
         // ---- the leaf reached, if any ----
