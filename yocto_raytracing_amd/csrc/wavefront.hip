@@ -337,7 +337,10 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene
 // samples are whole pixels, so the ordered per-pixel sum of k_accumulate is done here
 // from LDS and the per-sample radiance never goes to HBM.
 template <bool COUNT, bool FUSE>
-__global__ __launch_bounds__(WF_BLOCK) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
+#ifndef YRT_SHADE_WAVES
+#define YRT_SHADE_WAVES 5  // k_shade register budget (its natural 96 VGPRs; A/B: 6 -> +26 %, 8 -> +140 % from spills)
+#endif
+__global__ __launch_bounds__(WF_BLOCK, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
     const int n = level ? B.count[level] : nsamp_level0;
