@@ -48,6 +48,9 @@ constexpr int WF_BLOCK = 256;
 #define YRT_PF2 1  // closest hit: packet_first (goto-structured walk) instead of packet_trace<false>
 #endif
 constexpr int MAX_LEVELS = 16;
+#ifndef YRT_LEVEL_PRUNE
+#define YRT_LEVEL_PRUNE 1  // reflective scenes: stop launching levels once one spawns no ray
+#endif
 constexpr int TILE = 8;  // pixel tiles of 8x8 in the sample enumeration
 
 struct wf_buffers {
@@ -580,7 +583,16 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     const int tiles_y = (A.tile_h + TILE - 1) / TILE;
     const long long npix_total = (long long)tiles_x * tiles_y * TILE * TILE;
     const int nlevels = ds.reflective ? std::min(std::max(A.max_depth, 1), MAX_LEVELS) : 1;
-    const long long target = ds.reflective ? (1ll << 23) : (1ll << 27);
+    // samples per chunk: a whole frame at the BASELINE configs. A reflective scene keeps
+    // per-level buffers for every level (~100 B per sample and level), so its chunk is
+    // halved until the workspace takes at most half of the free HBM.
+    long long target = ds.reflective ? (1ll << 25) : (1ll << 27);
+    if (ds.reflective) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        free_b += ds.work_bytes;  // the current workspace is given back if it is regrown
+        while (target > (1ll << 20) && workspace_bytes((int)target, ds.nlights, nlevels) > free_b / 2) target /= 2;
+    }
     int pix_per_chunk = (int)std::max<long long>(1, std::min<long long>(npix_total, target / spp));
     pix_per_chunk = ((pix_per_chunk + TILE * TILE - 1) / (TILE * TILE)) * TILE * TILE;
     const int cap = pix_per_chunk * spp;
@@ -613,7 +625,21 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         int t = T.begin(phase_primary, stream);
         hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, C, B, counters);
         T.end(t, stream);
+        // levels run: a level with no mirror rays ends the chunk's recursion (the host reads
+        // the next level's ray count once per level; the per-level launches it saves cost
+        // more than the read)
+        int levels_run = nlevels;
         for (int level = 0; level < nlevels; level++) {
+            if (level > 0 && YRT_LEVEL_PRUNE) {
+                int cnt = 0;
+                hipError_t e = hipMemcpyAsync(&cnt, B.count + level, sizeof(int), hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(stream);
+                if (e != hipSuccess) return e;
+                if (cnt == 0) {
+                    levels_run = level;
+                    break;
+                }
+            }
             if (level > 0) {
                 t = T.begin(phase_bounce, stream);
                 hipLaunchKernelGGL((k_bounce<COUNT, PACKET, SE>), dim3(stride_grid), dim3(WF_BLOCK), 0, stream, ds.view,
@@ -640,7 +666,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                    stream, ds.view, A, level, nsamp, A.max_depth, B, counters, C, out);
             T.end(t, stream);
         }
-        for (int level = nlevels - 2; level >= 0; level--) {
+        for (int level = levels_run - 2; level >= 0; level--) {
             t = T.begin(phase_fold, stream);
             hipLaunchKernelGGL(k_fold_children, dim3(stride_grid), dim3(WF_BLOCK), 0, stream, level, B);
             T.end(t, stream);
