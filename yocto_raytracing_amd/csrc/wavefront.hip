@@ -48,6 +48,9 @@ constexpr int WF_BLOCK = 256;
 #define YRT_PF2 1  // closest hit: packet_first (goto-structured walk) instead of packet_trace<false>
 #endif
 constexpr int MAX_LEVELS = 16;
+#ifndef YRT_CHUNK_LOG2
+#define YRT_CHUNK_LOG2 29  // samples per chunk, non-reflective scenes (~70 B of HBM each)
+#endif
 #ifndef YRT_LEVEL_PRUNE
 #define YRT_LEVEL_PRUNE 1  // reflective scenes: stop launching levels once one spawns no ray
 #endif
@@ -583,11 +586,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     const int tiles_y = (A.tile_h + TILE - 1) / TILE;
     const long long npix_total = (long long)tiles_x * tiles_y * TILE * TILE;
     const int nlevels = ds.reflective ? std::min(std::max(A.max_depth, 1), MAX_LEVELS) : 1;
-    // samples per chunk: a whole frame at the BASELINE configs. A reflective scene keeps
-    // per-level buffers for every level (~100 B per sample and level), so its chunk is
+    // samples per chunk: a whole frame at c3/c4, 15 chunks at c5. A reflective scene keeps
+    // per-level buffers for every level (~100 B per sample and level). The chunk is
     // halved until the workspace takes at most half of the free HBM.
-    long long target = ds.reflective ? (1ll << 25) : (1ll << 27);
-    if (ds.reflective) {
+    long long target = ds.reflective ? (1ll << 25) : (1ll << YRT_CHUNK_LOG2);
+    {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         free_b += ds.work_bytes;  // the current workspace is given back if it is regrown
