@@ -525,7 +525,7 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
 #ifndef YRT_WI_LDS
 #define YRT_WI_LDS 1  // closest hit: the world 1/d kept in LDS across instance leaves (A/B: primary -1 %)
 #endif
-constexpr int packet_block = 256;  // threads per block of every kernel that runs packet_first
+constexpr int packet_block = 256;  // >= threads per block of every kernel that runs packet_first
 
 #ifndef YRT_FIRST_OCTANT
 #define YRT_FIRST_OCTANT 1  // closest hit: octant-specialised slab tests (see box_oct)

@@ -35,6 +35,20 @@ namespace yrt {
 namespace {
 
 constexpr int WF_BLOCK = 256;
+#ifndef YRT_PRIMARY_BLOCK
+#define YRT_PRIMARY_BLOCK 64  // threads per k_primary block (<= packet_block; a multiple of 64). A/B at c4: 256 -> 64 is -3 %
+#endif
+#ifndef YRT_SHADOW_BLOCK
+#define YRT_SHADOW_BLOCK 64
+#endif
+// threads per block of the packet shadow kernel: one wave. Walks of very different
+// lengths share a CU; a block's slots are only refilled once all its waves are done, so
+// the smallest block keeps the CU fullest (A/B at c4: 256 -> 64 is -5 % on k_shadow;
+// 1024 is +22 %). k_primary stays at WF_BLOCK: its LDS (the parked world 1/d) and the
+// per-block counter flush would cap the blocks per CU. The per-lane walks keep WF_BLOCK
+// (their stacks are in LDS).
+template <bool PACKET>
+constexpr int shadow_block() { return PACKET ? YRT_SHADOW_BLOCK : WF_BLOCK; }
 #ifndef YRT_TRACE_WAVES
 #define YRT_TRACE_WAVES 8  // waves per SIMD the traversal kernels are register-budgeted for (A/B at c4 with the structured walks: 7 -> 8 is -3.5 %)
 #endif
@@ -108,10 +122,10 @@ __device__ __forceinline__ void flush(unsigned long long* counters, int idx, uns
 // the timed kernels' counters: wave sums combined per block in LDS, then ONE device
 // atomic per counter per block into the block's counter line (a per-wave atomic
 // costs ~4x as many fabric atomics; the c4 shadow pass has 1.5 M blocks)
-template <int N>
+template <int N, int BS = WF_BLOCK>
 __device__ __forceinline__ void flush_block(unsigned long long* counters, const int (&idx)[N],
                                             const unsigned long long (&v)[N]) {
-    __shared__ unsigned long long part[WF_BLOCK / 64][N];
+    __shared__ unsigned long long part[BS / 64][N];
     const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < N; k++) {
@@ -122,7 +136,7 @@ __device__ __forceinline__ void flush_block(unsigned long long* counters, const 
     if (threadIdx.x < N) {
         unsigned long long t = 0;
 #pragma unroll
-        for (int q = 0; q < WF_BLOCK / 64; q++) t += part[q][threadIdx.x];
+        for (int q = 0; q < BS / 64; q++) t += part[q][threadIdx.x];
         const unsigned b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
         if (t) atomicAdd(counters + (size_t)(b % cnt_slots) * cnt_count + idx[threadIdx.x], t);
     }
@@ -212,11 +226,13 @@ __device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
 
 // ---- level 0: camera rays + closest hit + surface ----
 template <bool COUNT, bool PACKET, typename SE>
-__global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A, chunk_args C,
-                                                      wf_buffers B, unsigned long long* counters) {
+__global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A,
+                                                               chunk_args C, wf_buffers B,
+                                                               unsigned long long* counters) {
+    constexpr int BS = YRT_PRIMARY_BLOCK;
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
-    const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * WF_BLOCK + threadIdx.x;
+    const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
     const int nsamp = C.npix * C.spp;
     work_counts wc;
     bool valid = false;
@@ -243,7 +259,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene
         }
         store_surface(B, idx, hit, sf);
     }
-    flush_block<2>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
+    flush_block<2, BS>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
     if (COUNT) flush_work(counters, wc);
 }
 
@@ -286,8 +302,10 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
 // WIDE: the 4-wide any-hit walk (timed kernels on scenes whose wide stack fits);
 // otherwise the tracer's binary walk (and always for the instrumented COUNT pass)
 template <bool COUNT, bool PACKET, typename SE, bool WIDE>
-__global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene_view S, int level, int nsamp_level0, wf_buffers B,
-                                                     unsigned long long* counters) {
+__global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_shadow(dev_scene_view S, int level,
+                                                                     int nsamp_level0, wf_buffers B,
+                                                                     unsigned long long* counters) {
+    constexpr int BS = shadow_block<PACKET>();
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
     const int n = level ? B.count[level] : nsamp_level0;
@@ -301,10 +319,10 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene
     const vec3f lp0 = xyz(ld4(lr + 4));
     work_counts wc;
     unsigned long long rays = 0;
-    const int stride = gridDim.x * WF_BLOCK;
+    const int stride = gridDim.x * BS;
     const int nround = (n + stride - 1) / stride;
     for (int round = 0; round < nround; round++) {
-        const int idx = round * stride + bx * WF_BLOCK + threadIdx.x;
+        const int idx = round * stride + bx * BS + threadIdx.x;
         bool valid = false;
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
         if (idx < n) {
@@ -328,7 +346,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADOW_WAVES) void k_shadow(dev_scene
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
     }
     // shadow rays are counted once, here; yrt_last_stats reports rays = cnt_rays + this
-    flush_block<1>(counters, {cnt_shadow_rays}, {rays});
+    flush_block<1, BS>(counters, {cnt_shadow_rays}, {rays});
     if (COUNT) {
         flush_work(counters, wc);
         flush<true>(counters, cnt_shadow_box_tests, wc.box);
@@ -626,7 +644,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (e != hipSuccess) return e;
         }
         int t = T.begin(phase_primary, stream);
-        hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, C, B, counters);
+        constexpr int TB = shadow_block<PACKET>();
+        const int tgrid = (nsamp + TB - 1) / TB;
+        hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
+                           dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
         T.end(t, stream);
         // levels run: a level with no mirror rays ends the chunk's recursion (the host reads
         // the next level's ray count once per level; the per-level launches it saves cost
@@ -650,13 +671,13 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 T.end(t, stream);
             }
             if (ds.nlights > 0) {
-                dim3 sg(level ? stride_grid : grid, ds.nlights);
+                dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
                 if (!COUNT && PACKET && ds.wide_ok)
-                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(WF_BLOCK), YRT_EXP_SHADOW_LDS,
+                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), YRT_EXP_SHADOW_LDS,
                                        stream, ds.view, level, nsamp, B, counters);
                 else
-                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, false>), sg, dim3(WF_BLOCK), YRT_EXP_SHADOW_LDS,
+                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, false>), sg, dim3(TB), YRT_EXP_SHADOW_LDS,
                                        stream, ds.view, level, nsamp, B, counters);
                 T.end(t, stream);
             }
