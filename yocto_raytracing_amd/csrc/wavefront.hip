@@ -360,25 +360,28 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 // FUSE (level 0 of a scene without mirrors, s*s dividing the block): the block's
 // samples are whole pixels, so the ordered per-pixel sum of k_accumulate is done here
 // from LDS and the per-sample radiance never goes to HBM.
-template <bool COUNT, bool FUSE>
+#ifndef YRT_SHADE_FUSE64
+#define YRT_SHADE_FUSE64 0  // 1: fused k_shade in one-wave blocks when a pixel fits (A/B: +9 %)
+#endif
 #ifndef YRT_SHADE_WAVES
 #define YRT_SHADE_WAVES 5  // k_shade register budget (its natural 96 VGPRs; A/B: 6 -> +26 %, 8 -> +140 % from spills)
 #endif
-__global__ __launch_bounds__(WF_BLOCK, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
+template <bool COUNT, bool FUSE, int SB = WF_BLOCK>
+__global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
     const int n = level ? B.count[level] : nsamp_level0;
-    __shared__ float4 fused_rad[FUSE ? WF_BLOCK : 1];
-    __shared__ int cmp_count[WF_BLOCK / 64], cmp_base[WF_BLOCK / 64];
+    __shared__ float4 fused_rad[FUSE ? SB : 1];
+    __shared__ int cmp_count[SB / 64], cmp_base[SB / 64];
     work_counts wc;
     unsigned long long truncated = 0;
     const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
     const vec3f cam_o = {A.cam.ox, A.cam.oy, A.cam.oz};
     // the loop bound is uniform per wave so every lane reaches the ballot below
-    const int stride = gridDim.x * WF_BLOCK;
+    const int stride = gridDim.x * SB;
     const int nround = (n + stride - 1) / stride;
     for (int round = 0; round < nround; round++) {
-        const int idx = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
+        const int idx = round * stride + blockIdx.x * SB + threadIdx.x;
         bool spawn = false;
         vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0}, rec_kr = {0, 0, 0};
         if (idx < n) {
@@ -473,9 +476,9 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADE_WAVES) void k_shade(dev_scene_v
         __syncthreads();
         if (threadIdx.x == 0) {
             int tot = 0;
-            for (int q = 0; q < WF_BLOCK / 64; q++) tot += cmp_count[q];
+            for (int q = 0; q < SB / 64; q++) tot += cmp_count[q];
             int acc = tot ? atomicAdd(B.count + level + 1, tot) : 0;
-            for (int q = 0; q < WF_BLOCK / 64; q++) cmp_base[q] = acc, acc += cmp_count[q];
+            for (int q = 0; q < SB / 64; q++) cmp_base[q] = acc, acc += cmp_count[q];
         }
         __syncthreads();
         if (spawn) {
@@ -490,9 +493,9 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_SHADE_WAVES) void k_shade(dev_scene_v
     if (FUSE) {
         // raytrace.cpp:232-249: s*s samples of a pixel summed in jj/ii order, then / s*s
         __syncthreads();
-        const int ppb = WF_BLOCK / C.spp;
+        const int ppb = SB / C.spp;
         if ((int)threadIdx.x < ppb) {
-            const int pl = (int)(blockIdx.x * WF_BLOCK / C.spp) + threadIdx.x;
+            const int pl = (int)(blockIdx.x * SB / C.spp) + threadIdx.x;
             int lx, ly, i, j;
             const bool valid = pl < C.npix && pixel_of(A, C.tiles_x, C.pix0 + pl, lx, ly, i, j);
             if (pl < C.npix && lx < A.tile_w && ly < A.tile_h) {
@@ -631,7 +634,9 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
     // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE)
 #ifndef YRT_NO_FUSE
-    const bool fuse = nlevels == 1 && WF_BLOCK % spp == 0;
+    // fused shade blocks of one wave when a pixel's samples fit (s <= 8), else of WF_BLOCK
+    const int fuse_block = (YRT_SHADE_FUSE64 && 64 % spp == 0) ? 64 : WF_BLOCK;
+    const bool fuse = nlevels == 1 && fuse_block % spp == 0;
 #else
     const bool fuse = false;
 #endif
@@ -683,7 +688,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             }
             t = T.begin(phase_shade, stream);
             if (fuse)
-                hipLaunchKernelGGL((k_shade<COUNT, true>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, level,
+if (fuse_block == 64)
+                    hipLaunchKernelGGL((k_shade<COUNT, true, 64>), dim3((nsamp + 63) / 64), dim3(64), 0, stream, ds.view, A, level,
+                                   nsamp, A.max_depth, B, counters, C, out);
+                else
+                    hipLaunchKernelGGL((k_shade<COUNT, true>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, level,
                                    nsamp, A.max_depth, B, counters, C, out);
             else
                 hipLaunchKernelGGL((k_shade<COUNT, false>), dim3(level ? stride_grid : grid), dim3(WF_BLOCK), 0,
