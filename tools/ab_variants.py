@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
 import statistics
@@ -70,13 +71,16 @@ def main():
             out = torch.empty((h.value, w.value, 4), dtype=torch.float32, device="cuda")
         runs.append((Path(path).name, lib, N, ds, p, torch.cuda.Stream()))
     res = {name: {} for name, *_ in runs}
+    digest = {}
     for r in range(a.rounds + 1):  # round 0 = warmup
         for name, lib, N, ds, p, stream in runs:
             rc = lib.yrt_render(ds, C.byref(p), C.c_void_p(out.data_ptr()), 1, C.c_void_p(stream.cuda_stream))
             assert rc == 0, lib.yrt_last_error()
             t = N.Timings()
             lib.yrt_last_timings(ds, C.byref(t))
-            if r == 0:
+            if r == 0:  # warmup; the image digest shows whether the variants agree bit for bit
+                stream.synchronize()
+                digest[name] = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:16]
                 continue
             for k, ph in enumerate(N.PHASES):
                 if t.launches[k]:
@@ -92,7 +96,7 @@ def main():
     summary = {}
     for name, d in res.items():
         summary[name] = {ph: {"median": statistics.median(v), "min": min(v)} for ph, v in d.items()}
-        print(name, {ph: round(v["median"], 2) for ph, v in summary[name].items()})
+        print(name, {ph: round(v["median"], 2) for ph, v in summary[name].items()}, "image", digest[name])
     print(json.dumps(summary))
 
 

@@ -208,14 +208,26 @@ __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, fl
 // intersect_triangle (scene.cpp:229-263) without branches: the same values in the
 // same order; the early returns become one predicate (a NaN w1/w2/t passes its
 // range checks exactly as it does in the reference)
+#ifndef YRT_TRI_RCP
+#define YRT_TRI_RCP 1  // 1: the any-hit walk's 1/den as rcp_nr when in range (A/B: shadow -0.8 %)
+#endif
+// `in`: the lanes whose result is used. 1/den is the reference's IEEE division; with RCP,
+// when every such lane has den and 1/den normal (a wave-uniform check), fast_div.h's
+// rcp_nr gives the same bits in three instructions instead of ten. The closest-hit walk
+// does not gain from it (+0.6 %), the any-hit walk does.
+template <bool RCP = false>
 __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float tmax, vec3f v0, vec3f e1, vec3f e2,
-                                           float& t, float& w1, float& w2) {
+                                           float& t, float& w1, float& w2, bool in) {
     vec3f r = cross(d, e2);
     float den = dot(r, e1);
 #ifdef YRT_EXP_FASTTRI  // timing diagnostic only: approximate reciprocal (results differ)
     float inv_den = __builtin_amdgcn_rcpf(den);
 #else
-    float inv_den = 1.0f / den;
+    float inv_den;
+    if (!RCP || ballot(in && !rcp_nr_ok(den)))
+        inv_den = 1.0f / den;
+    else
+        inv_den = rcp_nr(den);
 #endif
     vec3f c = o - v0;
     w1 = dot(r, c) * inv_den;
@@ -328,7 +340,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     float t, w1, w2;
                     bool h;
                     if (kind == kind_triangles) {
-                        h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2);
+                        h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2, in);
                     } else {
                         // lines: ew = {1-s, s, 0, 0}; points: {1, 0, 0, 0} -- both are
                         // {1-w1-w2, w1, w2, 0} with w1 = ew.y, w2 = ew.z
@@ -677,7 +689,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                         if (COUNT && (me & 1)) wc.wprim++;
                         float t, w1, w2;
                         const bool h =
-                            tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2) && in;
+                            tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, in) && in;
                         tmax = h ? t : tmax;
                         hslot = h ? cur_slot : hslot;
                         hei = h ? ibits(pv[0].w) : hei;
@@ -766,6 +778,10 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     hr.dist = tmax;
     return true;
 }
+
+#ifndef YRT_LEAF_EARLY
+#define YRT_LEAF_EARLY 0  // any hit: leave a leaf once every lane in it is occluded
+#endif
 
 #ifndef YRT_WIDE_SKIP
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
@@ -923,8 +939,12 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                         float4 pv[3];
                         ld_records<3>(S.sprims + 3 * i, pv);
                         float t, w1, w2;
-                        const bool h = tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2);
+                        const bool h =
+                            tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, inl);
                         leaf_hit |= (h && inl) ? 1 : 0;
+                        // every lane of the leaf occluded: the leaf's other triangles cannot
+                        // change the answer
+                        if (YRT_LEAF_EARLY && !(mask & ~ballot(leaf_hit != 0))) break;
                     }
                 } else {
                     for (int i = first; i < first + count; i++) {
