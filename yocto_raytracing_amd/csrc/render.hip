@@ -84,10 +84,10 @@ __device__ vec3f shade_path(const dev_scene_view& S, const dev_render_args& A, r
                 float sinnl = __builtin_sqrtf(1.0f - prodnl);
                 float sinnh = __builtin_sqrtf(1.0f - prodnh);
                 ld = ld * sinnl;
-                ls = ls * powf_cr(sinnh, ns);
+                ls = ls * spec_pow(sinnh, ns, ls);
             } else {
                 ld = ld * smax(0.0f, dot(sf.n, l));
-                ls = ls * powf_cr(smax(0.0f, dot(sf.n, h)), ns);
+                ls = ls * spec_pow(smax(0.0f, dot(sf.n, h)), ns, ls);
             }
             c = c + (ld + ls);
         }

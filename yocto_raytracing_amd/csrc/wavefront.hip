@@ -434,10 +434,10 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                         float sinnl = __builtin_sqrtf(1.0f - prodnl);
                         float sinnh = __builtin_sqrtf(1.0f - prodnh);
                         ld = ld * sinnl;
-                        ls = ls * powf_cr(sinnh, ns);
+                        ls = ls * spec_pow(sinnh, ns, ls);
                     } else {
                         ld = ld * smax(0.0f, dot(nrm, l));
-                        ls = ls * powf_cr(smax(0.0f, dot(nrm, h)), ns);
+                        ls = ls * spec_pow(smax(0.0f, dot(nrm, h)), ns, ls);
                     }
                     c = c + (ld + ls);
                 }
