@@ -208,6 +208,9 @@ __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, fl
 // intersect_triangle (scene.cpp:229-263) without branches: the same values in the
 // same order; the early returns become one predicate (a NaN w1/w2/t passes its
 // range checks exactly as it does in the reference)
+#ifndef YRT_TRI_RCP_FIRST
+#define YRT_TRI_RCP_FIRST 0  // the same in the closest-hit walk (A/B: primary +0.6 %)
+#endif
 #ifndef YRT_TRI_RCP
 #define YRT_TRI_RCP 1  // 1: the any-hit walk's 1/den as rcp_nr when in range (A/B: shadow -0.8 %)
 #endif
@@ -689,7 +692,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                         if (COUNT && (me & 1)) wc.wprim++;
                         float t, w1, w2;
                         const bool h =
-                            tri_hit_nb(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, in) && in;
+                            tri_hit_nb<YRT_TRI_RCP_FIRST>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, in) && in;
                         tmax = h ? t : tmax;
                         hslot = h ? cur_slot : hslot;
                         hei = h ? ibits(pv[0].w) : hei;
