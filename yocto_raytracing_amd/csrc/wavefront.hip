@@ -363,10 +363,15 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #ifndef YRT_SHADE_FUSE64
 #define YRT_SHADE_FUSE64 0  // 1: fused k_shade in one-wave blocks when a pixel fits (A/B: +9 %)
 #endif
+#ifndef YRT_SHADE_OCC4
+#define YRT_SHADE_OCC4 1  // k_shade: occlusion bytes of <= 4 lights loaded with the surface
+#endif
 #ifndef YRT_SHADE_WAVES
 #define YRT_SHADE_WAVES 5  // k_shade register budget (its natural 96 VGPRs; A/B: 6 -> +26 %, 8 -> +140 % from spills)
 #endif
-template <bool COUNT, bool FUSE, int SB = WF_BLOCK>
+// OCC4 (scenes with at most four lights): the occlusion bytes are loaded together with the
+// surface, one memory round trip instead of one per light inside the light loop.
+template <bool COUNT, bool FUSE, int SB = WF_BLOCK, bool OCC4 = false>
 __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
@@ -386,6 +391,15 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
         vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0}, rec_kr = {0, 0, 0};
         if (idx < n) {
             float4 s0 = ld4(B.surf0 + idx);
+            uint32_t occ_bits = 0;
+            if constexpr (OCC4) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int lq = q < S.nlights ? q : 0;  // an unconditional load, masked after
+                    const uint32_t ob = B.occl[(size_t)lq * B.capacity + idx];
+                    occ_bits |= (q < S.nlights && ob != 0u) ? 1u << q : 0u;
+                }
+            }
             const int info = ibits(s0.w);
             vec3f R = {0, 0, 0};
             bool write_r = info != -2;
@@ -413,7 +427,7 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 // raytrace.cpp:147 (per light) and :196 (mirror): the same value each time
                 const vec3f v = normalize(ro - p);
                 for (int li = 0; li < S.nlights; li++) {
-                    if (B.occl[(size_t)li * B.capacity + idx]) continue;
+                    if (OCC4 ? ((occ_bits >> li) & 1u) != 0u : B.occl[(size_t)li * B.capacity + idx] != 0) continue;
                     const f4* lr = S.lights + 6 * li;
                     frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
                     vec3f lp0 = xyz(ld4(lr + 4)), ke = xyz(ld4(lr + 5));
@@ -687,16 +701,25 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 T.end(t, stream);
             }
             t = T.begin(phase_shade, stream);
-            if (fuse)
-if (fuse_block == 64)
-                    hipLaunchKernelGGL((k_shade<COUNT, true, 64>), dim3((nsamp + 63) / 64), dim3(64), 0, stream, ds.view, A, level,
-                                   nsamp, A.max_depth, B, counters, C, out);
+            const bool occ4 = YRT_SHADE_OCC4 && ds.nlights <= 4;
+#define YRT_SHADE_LAUNCH(FU, SBV, GRID)                                                                          \
+    do {                                                                                                        \
+        if (occ4)                                                                                               \
+            hipLaunchKernelGGL((k_shade<COUNT, FU, SBV, true>), GRID, dim3(SBV), 0, stream, ds.view, A, level, nsamp, \
+                               A.max_depth, B, counters, C, out);                                               \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_shade<COUNT, FU, SBV, false>), GRID, dim3(SBV), 0, stream, ds.view, A, level,      \
+                               nsamp, A.max_depth, B, counters, C, out);                                        \
+    } while (0)
+            if (fuse) {
+                if (fuse_block == 64)
+                    YRT_SHADE_LAUNCH(true, 64, dim3((nsamp + 63) / 64));
                 else
-                    hipLaunchKernelGGL((k_shade<COUNT, true>), dim3(grid), dim3(WF_BLOCK), 0, stream, ds.view, A, level,
-                                   nsamp, A.max_depth, B, counters, C, out);
-            else
-                hipLaunchKernelGGL((k_shade<COUNT, false>), dim3(level ? stride_grid : grid), dim3(WF_BLOCK), 0,
-                                   stream, ds.view, A, level, nsamp, A.max_depth, B, counters, C, out);
+                    YRT_SHADE_LAUNCH(true, WF_BLOCK, dim3(grid));
+            } else {
+                YRT_SHADE_LAUNCH(false, WF_BLOCK, dim3(level ? stride_grid : grid));
+            }
+#undef YRT_SHADE_LAUNCH
             T.end(t, stream);
         }
         for (int level = levels_run - 2; level >= 0; level--) {
