@@ -363,6 +363,9 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #ifndef YRT_SHADE_FUSE64
 #define YRT_SHADE_FUSE64 0  // 1: fused k_shade in one-wave blocks when a pixel fits (A/B: +9 %)
 #endif
+#ifndef YRT_SHADE_SMAT
+#define YRT_SHADE_SMAT 0  // k_shade: a wave-uniform material record through the scalar cache (A/B: c4 shade +12 %)
+#endif
 #ifndef YRT_SHADE_OCC4
 #define YRT_SHADE_OCC4 1  // k_shade: occlusion bytes of <= 4 lights loaded with the surface
 #endif
@@ -410,8 +413,21 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 const vec2f uv = {s1.w, B.surfv[idx]};
                 const int mat = info >> 2, kind = info & 3;
                 const vec3f ro = level ? xyz(ld4(B.ray_o[level] + idx)) : cam_o;
-                float4 m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1);
-                float4 m2 = ld4(S.mats + 4 * mat + 2), m3 = ld4(S.mats + 4 * mat + 3);
+                float4 m0, m1, m2, m3;
+#if YRT_SHADE_SMAT
+                // a wave on one material (the usual case: a pixel's samples) reads its
+                // record through the scalar cache, one 64 B load
+                const int mat_w = __builtin_amdgcn_readfirstlane(mat);
+                if (__ballot(mat != mat_w) == 0) {
+                    float4 mr[4];
+                    ld_scalar_at<4>(S.mats, (unsigned)(4 * mat_w), mr);
+                    m0 = mr[0], m1 = mr[1], m2 = mr[2], m3 = mr[3];
+                } else
+#endif
+                {
+                    m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1);
+                    m2 = ld4(S.mats + 4 * mat + 2), m3 = ld4(S.mats + 4 * mat + 3);
+                }
                 const vec3f kd0 = xyz(m0), ks0 = xyz(m1), kr = xyz(m2);
                 const float ns = m0.w;
                 const int kd_txt = ibits(m1.w), ks_txt = ibits(m2.w);
