@@ -211,6 +211,9 @@ __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, fl
 #ifndef YRT_TRI_RCP_FIRST
 #define YRT_TRI_RCP_FIRST 0  // the same in the closest-hit walk (A/B: primary +0.6 %)
 #endif
+#ifndef YRT_TRI_EARLY
+#define YRT_TRI_EARLY 1  // triangle test: leave after w1 when no lane that counts passes it
+#endif
 #ifndef YRT_TRI_RCP
 #define YRT_TRI_RCP 1  // 1: the any-hit walk's 1/den as rcp_nr when in range (A/B: shadow -0.8 %)
 #endif
@@ -234,6 +237,14 @@ __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float t
 #endif
     vec3f c = o - v0;
     w1 = dot(r, c) * inv_den;
+#if YRT_TRI_EARLY
+    // no lane that counts passes the first barycentric test: the rest of the test (half of
+    // it) cannot make any of them hit
+    if (!ballot(in && (den != 0) && !(w1 < 0 || w1 > 1))) {
+        t = w2 = 0.0f;
+        return false;
+    }
+#endif
     vec3f s = cross(c, e1);
     w2 = dot(s, d) * inv_den;
     t = dot(s, e2) * inv_den;
