@@ -1,6 +1,7 @@
 // Exhaustive / sweep check of the division shortcuts in trace_common.h against the IEEE
 // division the reference performs (hipcc's correctly rounded 1.0f / x and a / b):
 //   rcp_nr(x)     for every one of the 2^32 f32 inputs x;
+//   sqrt_nr(x)    for every one of the 2^32 f32 inputs x (against sqrtf);
 //   div_nr(a, b)  for every positive a (2^31; the sign is symmetric) and a list of b.
 // Each mismatch class is counted (NaN results compare equal to NaN). Build and run:
 //   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -I yocto_raytracing_amd/csrc \
@@ -32,6 +33,19 @@ __global__ void k_rcp(unsigned long long base) {
         }
     } else {
         atomicAdd(&g_bad[1], 1ull);  // inputs left to the exact division
+    }
+}
+
+// every 32-bit pattern: sqrt_nr where sqrt_nr_ok admits it, against sqrtf
+__global__ void k_sqrt(unsigned long long base) {
+    const unsigned long long i = base + (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const float x = __uint_as_float((unsigned)i);
+    if (yrt::sqrt_nr_ok(x)) {
+        if (!same(yrt::sqrt_nr(x), __builtin_sqrtf(x))) {
+            if (atomicAdd(&g_bad[2], 1ull) == 0) g_first[2] = (unsigned)i;
+        }
+    } else {
+        atomicAdd(&g_bad[3], 1ull);
     }
 }
 
@@ -73,6 +87,15 @@ int main() {
     printf("rcp_nr: 2^32 inputs, %llu mismatches (first 0x%08x), %llu left to the division\n", bad[0], first[0],
            bad[1]);
     int fails = bad[0] != 0;
+
+    check(hipMemcpyToSymbol(HIP_SYMBOL(g_bad), z, sizeof z), "reset");
+    for (unsigned long long base = 0; base < n; base += (unsigned long long)blk * grid)
+        hipLaunchKernelGGL(k_sqrt, dim3(grid), dim3(blk), 0, 0, base);
+    check(hipDeviceSynchronize(), "k_sqrt");
+    check(hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof bad), "read");
+    check(hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof first), "read");
+    printf("sqrt_nr: 2^32 inputs, %llu mismatches (first 0x%08x), %llu left to sqrtf\n", bad[2], first[2], bad[3]);
+    fails |= bad[2] != 0;
 
     // b: around 1 (normalize divides by lengths of unit-ish vectors), then a spread
     float bs[64];

@@ -459,6 +459,9 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 #ifndef YRT_FAST_DIV
 #define YRT_FAST_DIV 1
 #endif
+#ifndef YRT_FAST_SQRT
+#define YRT_FAST_SQRT 1  // instance entry: normalize's sqrt as sqrt_nr when every lane admits it
+#endif
 
 // the instance-local direction and its inverse on instance entry (transform_ray_inverse,
 // vmath.h:275-278: the direction renormalized, invd = 1/d as intersect_check_bbox
@@ -482,13 +485,14 @@ __device__ __forceinline__ void enter_direction(const frame3f& f, vec3f wd, unsi
 #if YRT_FAST_DIV
     {
         const vec3f v = {dot(f.x, wd), dot(f.y, wd), dot(f.z, wd)};
-        const float l = length(v);
+        const float l2 = dot(v, v);  // length(v) = sqrt(dot(v, v))
+        const float l = YRT_FAST_SQRT ? sqrt_nr(l2) : __builtin_sqrtf(l2);
         const float y = rcp_nr(l);
         const vec3f c = v * y;
         const float lo = fminf(fminf(l, fabsf(c.x)), fminf(fabsf(c.y), fabsf(c.z)));
         const float hi = fmaxf(fmaxf(l, fabsf(c.x)), fmaxf(fabsf(c.y), fabsf(c.z)));
         // l == l: a NaN component makes l NaN (fminf/fmaxf would drop it)
-        const bool fast = (l == l) && lo >= 0x1p-126f && hi < 0x1p126f;
+        const bool fast = (l == l) && lo >= 0x1p-126f && hi < 0x1p126f && (!YRT_FAST_SQRT || sqrt_nr_ok(l2));
         if (!(ballot(!fast) & lanes)) {
             cd = c;
             ci = {rcp_nr(c.x), rcp_nr(c.y), rcp_nr(c.z)};
