@@ -214,8 +214,28 @@ __device__ __forceinline__ tracer<ANY, COUNT, PACKET, SE> make_tracer(traversal_
 // tiles trace neighbouring rays through the same BVH nodes, so each XCD's L2 (and each
 // CU's scalar cache) sees one region of the image instead of every eighth tile of all
 // of it. A bijection for any grid size.
+#ifndef YRT_XCD_CHUNK
+#define YRT_XCD_CHUNK 64  // YRT_XCD_REMAP 2: blocks per XCD run
+#endif
+// YRT_XCD_REMAP 2 keeps the round-robin sweep over the image but hands each XCD runs of
+// YRT_XCD_CHUNK consecutive blocks: the grid is cut into super-chunks of 8 runs, XCD x
+// takes run x of each (a bijection; a ragged last super-chunk keeps its blocks).
+template <unsigned C>
+__device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
+    constexpr unsigned G = 8u * C;
+    if (b >= n / G * G) return b;
+    const unsigned w = b % G;
+    return b - w + (w % 8u) * C + w / 8u;
+}
+
+#ifndef YRT_XCD_CHUNK_PRIMARY
+#define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (0: plain round robin)
+#endif
+
 __device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
-#if YRT_XCD_REMAP
+#if YRT_XCD_REMAP == 2
+    return xcd_runs<YRT_XCD_CHUNK>(b, n);
+#elif YRT_XCD_REMAP
     const unsigned x = b % 8u, j = b / 8u, q = n / 8u, r = n % 8u;
     return x * q + (x < r ? x : r) + j;
 #else
@@ -232,7 +252,11 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
     constexpr int BS = YRT_PRIMARY_BLOCK;
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
+#if YRT_XCD_CHUNK_PRIMARY && !YRT_XCD_REMAP
+    const int idx = (int)xcd_runs<YRT_XCD_CHUNK_PRIMARY>(blockIdx.x, gridDim.x) * BS + threadIdx.x;
+#else
     const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
+#endif
     const int nsamp = C.npix * C.spp;
     work_counts wc;
     bool valid = false;
