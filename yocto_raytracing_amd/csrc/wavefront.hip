@@ -68,7 +68,10 @@ constexpr int MAX_LEVELS = 16;
 #ifndef YRT_LEVEL_PRUNE
 #define YRT_LEVEL_PRUNE 1  // reflective scenes: stop launching levels once one spawns no ray
 #endif
-constexpr int TILE = 8;  // pixel tiles of 8x8 in the sample enumeration
+#ifndef YRT_TILE
+#define YRT_TILE 8
+#endif
+constexpr int TILE = YRT_TILE;  // pixel tiles of TILE x TILE in the sample enumeration
 
 struct wf_buffers {
     f4* surf0;          // {p.xyz, info}: info = mat*4+kind, -1 miss, -2 not a sample
