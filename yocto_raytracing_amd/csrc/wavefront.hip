@@ -231,6 +231,9 @@ __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
     return b - w + (w % 8u) * C + w / 8u;
 }
 
+#ifndef YRT_SHADOW_LIGHT_MINOR
+#define YRT_SHADOW_LIGHT_MINOR 24  // k_shadow: XCD run length with the light index minor (0: light-major round robin; A/B: shadow -1.1 %)
+#endif
 #ifndef YRT_XCD_CHUNK_PRIMARY
 #define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (0: plain round robin)
 #endif
@@ -338,9 +341,18 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     const int n = level ? B.count[level] : nsamp_level0;
     // level 0 (one block per 256 samples and light): the remap runs over the whole
     // (x, light) grid; levels >= 1 are grid-stride and keep their blocks
+#if YRT_SHADOW_LIGHT_MINOR
+    // a pixel block's lights in neighbouring blocks (light index minor), dealt in XCD runs
+    const unsigned lin = level ? blockIdx.x
+                               : xcd_runs<YRT_SHADOW_LIGHT_MINOR>(blockIdx.y * gridDim.x + blockIdx.x,
+                                                                  gridDim.x * gridDim.y);
+    const int li = level ? (int)blockIdx.y : (int)(lin % gridDim.y);
+    const int bx = level ? (int)blockIdx.x : (int)(lin / gridDim.y);
+#else
     const unsigned lin = level ? blockIdx.x : xcd_block(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int li = level ? (int)blockIdx.y : (int)(lin / gridDim.x);
     const int bx = level ? (int)blockIdx.x : (int)(lin % gridDim.x);
+#endif
     const f4* lr = S.lights + 6 * li;
     const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
     const vec3f lp0 = xyz(ld4(lr + 4));
