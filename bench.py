@@ -3,22 +3,33 @@
 MI355X GPUs of one node.
 
 One step = one full frame of the hot path (raytrace(), src/raytrace.cpp:213) over
-the resident scene, end to end: every rank renders its interleaved 8-row bands of
-the frame with the gfx950 kernel, then the float framebuffer is all-gathered over
-RCCL (xGMI) and every rank reassembles the image (the north_star's framebuffer gather);
-with RCCL the gather of frame i runs on a communication stream while frame i+1 renders.
-Total work is fixed as N grows ("scaling": "strong").
+the resident scene: every rank renders its interleaved 8-row bands of the frame with
+the gfx950 kernels, then the float framebuffer is all-gathered over RCCL (xGMI) and
+every rank reassembles the image (the north_star's framebuffer gather); with RCCL the
+gather of frame i runs on a communication stream while frame i+1 renders. Total work
+is fixed as N grows ("scaling": "strong").
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py --resolution 4096 --width 4096 --samples 16      # c5's frame
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-value   = all rays traced by all ranks (camera + shadow + reflection, the
-          reference's intersect_first + intersect_any calls) / wall time of K frames
-roofline: the render kernel's ALGORITHMIC bytes per launch (SURVEY §8d cost model x
-          the work counters of an instrumented, untimed pass) / its mean launch time
-          measured with HIP events on the launch stream, against 8 TB/s HBM
-cpu_baseline: the reference itself (oracle/_ref, compiled from the unmodified
-          sources) on a bounded sample of rows of the same frame, single thread
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches
+its own N ranks (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) before
+anything touches the GPU; rank 0 prints the one JSON line.
+
+value     all rays traced by all ranks (camera + shadow + reflection, the reference's
+          intersect_first + intersect_any calls) / wall time of K frames
+roofline  the dominant kernel (k_shadow at c4) is bound by instruction ISSUE, not by
+          HBM (its 2.9 MB scene is cache-resident): achieved = its scalar- or vector-
+          instruction count per launch (rocprofv3 SQ_INSTS_SALU / SQ_INSTS_VALU,
+          committed under profiles/, tools/gpu_issue_pmc.sh) / its mean launch time
+          measured live with HIP events on the launch stream, against the chip's issue
+          peak (one SALU per CU per clock; one wave64 VALU per SIMD per two clocks; 256
+          CUs at 2.4 GHz). The pipe with the higher fraction is the bound. The HBM
+          fraction from the FETCH_SIZE/WRITE_SIZE passes is reported beside it.
+cpu_baseline  the reference itself (oracle/_ref, compiled from the unmodified sources)
+          on a bounded sample of rows of the same frame, single thread; beside it the C
+          restatement (oracle/liboracle.so) on every host core given to this job
 """
 from __future__ import annotations
 
@@ -27,6 +38,8 @@ import ctypes
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -35,13 +48,19 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
+BASELINE_METRIC = "Mrays/sec + ms/frame, instance10000 1920×1080×64spp, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# algorithmic bytes of the reference's traversal on its own AoS layout
-BYTES_BOX, BYTES_INST, BYTES_PRIM, BYTES_HIT, BYTES_TEX, BYTES_PIXEL = 32, 56, 52, 216, 16, 16
+# issue peaks (MI355X_MICROARCH.md: 256 CUs, 4 SIMD-32 per CU, 2400 MHz max clock; a
+# wave64 VALU instruction issues over 2 clocks on its SIMD; one scalar unit per CU)
+N_CU, CLOCK_HZ = 256, 2.4e9
+SALU_PEAK = N_CU * 1.0 * CLOCK_HZ / 1e9   # G wave-instructions/s
+VALU_PEAK = N_CU * 4 * 0.5 * CLOCK_HZ / 1e9
 BAND = 8
+PHASE_KERNEL = {"primary": "k_primary<false, true, unsigned int>",
+                "shadow": "k_shadow<false, true, unsigned int, true>",
+                "shade": "k_shade<false, true, 256, true>",
+                "megakernel": "render_kernel<false>"}
 
 
 def parse():
@@ -53,11 +72,52 @@ def parse():
     p.add_argument("--resolution", type=int, default=1080)
     p.add_argument("--width", type=int, default=0)
     p.add_argument("--samples", type=int, default=8, help="per axis: 8 -> 64 spp")
-    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per leg (0 = skip)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    p.add_argument("--issue-json", default=str(ROOT / "profiles" / "issue_counters.json"))
     p.add_argument("--algorithm", default="wavefront", choices=("wavefront", "megakernel", "wavefront_lane"))
+    p.add_argument("--dry-run", action="store_true",
+                   help="launch/rendezvous/report only, no GPU work (tests the N-rank launcher on CPU)")
     return p.parse_args()
 
+
+# ---------------------------------------------------------------- rank launcher
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """One process per GPU, started from this process before it touches the GPU (it
+    never initialises HIP: `import torch` does not). Rank 0 prints the JSON line."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:  # a failed rank ends the job: stop the others
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            q.kill()
+    return rc
+
+
+# ---------------------------------------------------------------- CPU baselines
 
 def cpu_model() -> str:
     try:
@@ -69,12 +129,26 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(scene_file: Path, res: int, spp_axis: int, budget_s: float):
-    """The reference's own code (oracle/_ref/libyrtref.so) on rows of the same frame.
-    Falls back to the C restatement (oracle/liboracle.so, 1 thread) if the reference
-    build did not travel. Test/baseline infrastructure only."""
+def _timed_rows(run, H: int, budget_s: float, threads: int = 1):
+    """calibrate on the middle row, then time evenly spaced rows filling about
+    `budget_s` of wall time on `threads` threads (at least one row per thread)"""
+    t0 = time.perf_counter()
+    run(np.array([H // 2], np.int32))
+    t1 = time.perf_counter() - t0
+    nrows = max(threads, min(H, int(budget_s * threads / max(t1, 1e-6))))
+    rows = np.linspace(0, H - 1, nrows).astype(np.int32)
+    t0 = time.perf_counter()
+    rays = run(rows)
+    el = time.perf_counter() - t0
+    return rows, rays, el
+
+
+def cpu_baseline(scene_file: Path, res: int, width: int, spp_axis: int, budget_s: float):
+    """The reference's own code (oracle/_ref/libyrtref.so, single thread) on rows of the
+    same frame; the C restatement (1 thread) if the reference build did not travel.
+    Test/baseline infrastructure only."""
     ref_so = ROOT / "oracle" / "_ref" / "libyrtref.so"
-    if ref_so.exists():
+    if ref_so.exists() and not width:
         lib = ctypes.CDLL(str(ref_so))
         lib.ref_read_scene.restype = ctypes.c_void_p
         lib.ref_read_scene.argtypes = [ctypes.c_char_p]
@@ -93,25 +167,14 @@ def cpu_baseline(scene_file: Path, res: int, spp_axis: int, budget_s: float):
             return lib.ref_render_rows(scn, 0.1, res, spp_axis, r.ctypes.data, len(r), out.ctypes.data)
         kind = "reference"
     else:
-        sys.path.insert(0, str(ROOT / "tests"))
-        from helpers import Oracle  # test infrastructure, baseline leg only
-
-        os.environ["OMP_NUM_THREADS"] = "1"
-        o = Oracle(str(scene_file))
+        o = _oracle(scene_file, 1)
         W, H = o.image_size(res)
+        W = width or W
 
         def run(rows):
-            return o.render(res, spp_axis, rows=rows)[1]
+            return o.render(res, spp_axis, rows=rows, width=width)[1]
         kind = "port"
-    # calibrate on the middle row, then sample evenly spaced rows to fill the budget
-    t0 = time.perf_counter()
-    rays = run([H // 2])
-    t1 = time.perf_counter() - t0
-    nrows = max(1, min(H, int(budget_s / max(t1, 1e-6))))
-    rows = np.linspace(0, H - 1, nrows).astype(np.int32)
-    t0 = time.perf_counter()
-    rays = run(rows)
-    el = time.perf_counter() - t0
+    rows, rays, el = _timed_rows(run, H, budget_s)
     samples = len(rows) * W * spp_axis * spp_axis
     return {
         "value": rays / el / 1e6,
@@ -124,23 +187,96 @@ def cpu_baseline(scene_file: Path, res: int, spp_axis: int, budget_s: float):
     }
 
 
+def _oracle(scene_file: Path, threads: int):
+    sys.path.insert(0, str(ROOT / "tests"))
+    from helpers import Oracle, oracle_lib  # test infrastructure, baseline legs only
+
+    lib = oracle_lib()
+    lib.oracle_set_threads.restype = ctypes.c_int
+    lib.oracle_set_threads.argtypes = [ctypes.c_int]
+    lib.oracle_set_threads(threads)
+    return Oracle(str(scene_file))
+
+
+def cpu_baseline_all_cores(scene_file: Path, res: int, width: int, spp_axis: int, budget_s: float):
+    """The C restatement (oracle.c, OpenMP over rows) on every core this job has:
+    OMP_NUM_THREADS when the host sets it (16 per GPU on the GPU box), else all CPUs."""
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    o = _oracle(scene_file, cores)
+    W, H = o.image_size(res)
+    W = width or W
+
+    def run(rows):
+        return o.render(res, spp_axis, rows=rows, width=width)[1]
+    rows, rays, el = _timed_rows(run, H, budget_s, threads=cores)
+    o.lib.oracle_set_threads(1)
+    samples = len(rows) * W * spp_axis * spp_axis
+    return {
+        "value": rays / el / 1e6,
+        "unit": "Mrays/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"{len(rows)} evenly spaced rows x {W} px x {spp_axis * spp_axis} spp ({samples} camera "
+                   f"samples, {rays} rays) in {el:.1f} s on {cores} threads of {cpu_model()} "
+                   f"(oracle/oracle.c, OpenMP over rows)"),
+    }
+
+
+# ---------------------------------------------------------------- roofline
+
+def issue_roofline(issue_json: Path, key: str, kernel_ms: float):
+    """achieved issue rate of the dominant kernel: its committed per-launch instruction
+    counts / the live launch time"""
+    try:
+        rec = json.loads(issue_json.read_text()).get(key)
+    except (OSError, ValueError):
+        rec = None
+    if not rec or kernel_ms <= 0:
+        return None
+    s = kernel_ms / 1e3
+    salu = rec["SQ_INSTS_SALU"] / s / 1e9
+    valu = rec["SQ_INSTS_VALU"] / s / 1e9
+    pipes = {"salu": {"achieved": salu, "peak": SALU_PEAK, "frac": salu / SALU_PEAK},
+             "valu": {"achieved": valu, "peak": VALU_PEAK, "frac": valu / VALU_PEAK}}
+    bound = max(pipes, key=lambda k: pipes[k]["frac"])
+    return bound, pipes, rec
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+
+    backend = os.environ.get("YRT_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
+    if a.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo" if backend == "gloo" else backend)
+            t = torch.tensor([float(rank)])
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world,
+                              "rank_sum": world * (world - 1) / 2 if world > 1 else 0.0,
+                              "checked_sum": float(t[0]) if world > 1 else 0.0}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     # rehearsal of the N-rank path on fewer GPUs (e.g. 2 ranks on one card with gloo):
     # YRT_BENCH_DEVICES=1 maps rank r to device r % 1; the driver's runs never set it
     ndev_override = int(os.environ.get("YRT_BENCH_DEVICES", "0"))
     if ndev_override > 0:
         local = local % ndev_override
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N>1 needs one process per GPU: launch with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("YRT_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -163,45 +299,18 @@ def main():
     params.tile_h = local_rows  # every rank renders the same padded count (rows past H read 0)
     # two frames in flight at N > 1 over RCCL: frame i's all_gather + reassembly run on a
     # communication stream while frame i+1 renders (double-buffered shards and frames)
-    overlap = world > 1 and (dist.get_backend() == "nccl" or os.environ.get("YRT_BENCH_OVERLAP") == "1")
+    backend_name = dist.get_backend() if world > 1 else None
+    overlap = world > 1 and (backend_name == "nccl" or os.environ.get("YRT_BENCH_OVERLAP") == "1")
     nbuf = 2 if overlap else 1
     shards = [torch.empty((local_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     gathered = [torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
                 for _ in range(nbuf)]
     frames = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
-    shard = shards[0]
     index = torch.as_tensor(layout.gather_index(), device=dev)
     stream = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev) if overlap else None
     rendered = [torch.cuda.Event() for _ in range(nbuf)]
     gathered_ev = [None] * nbuf
-
-    # untimed instrumented pass: algorithmic work counts for the roofline bytes
-    pc = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, band=band, count_work=True,
-                           algorithm=a.algorithm)
-    pc.tile_h = local_rows
-    ds.render_into(pc, shard.data_ptr(), stream=stream.cuda_stream)
-    work = ds.last_stats()
-    # per kernel phase: SURVEY §8d cost model on the phase's own traversal counts, plus
-    # the wavefront buffers the phase reads/writes (shadow: 16 B hit point in, 1 B out)
-    sh = {k: work[f"shadow_{k}"] for k in ("box_tests", "instance_entries", "prim_tests", "rays")}
-    alg = {
-        "shadow": sh["box_tests"] * BYTES_BOX + sh["instance_entries"] * BYTES_INST +
-                  sh["prim_tests"] * BYTES_PRIM + sh["rays"] * 17,
-        "primary": (work["box_tests"] - sh["box_tests"]) * BYTES_BOX +
-                   (work["instance_entries"] - sh["instance_entries"]) * BYTES_INST +
-                   (work["prim_tests"] - sh["prim_tests"]) * BYTES_PRIM + work["camera_samples"] * 36,
-        "megakernel": work["box_tests"] * BYTES_BOX + work["instance_entries"] * BYTES_INST +
-                      work["prim_tests"] * BYTES_PRIM + work["shaded_hits"] * BYTES_HIT +
-                      work["texture_lookups"] * BYTES_TEX + local_rows * W * BYTES_PIXEL,
-    }
-    # rocprof names of the timed (COUNT=false) kernels: <COUNT, PACKET, stack entry>
-    targs = {"wavefront": "<false, true, unsigned int>", "wavefront_lane": "<false, false, unsigned short>"}
-    kernel_names = {"megakernel": "render_kernel<false>"}
-    for ph in ("primary", "shadow", "bounce"):
-        kernel_names[ph] = f"k_{ph}{targs.get(a.algorithm, '')}"
-    if a.algorithm == "wavefront":  # the timed shadow kernel walks the 4-wide collapse
-        kernel_names["shadow"] = "k_shadow<false, true, unsigned int, true>"
 
     def step(i, timing=0):
         b = i % nbuf
@@ -209,7 +318,7 @@ def main():
         if not overlap:
             ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
             gather_frame(shards[b], layout, index, gathered[b], frames[b])
-            return
+            return b
         if gathered_ev[b] is not None:  # shards[b] is free once its previous gather has read it
             stream.wait_event(gathered_ev[b])
         ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
@@ -219,6 +328,7 @@ def main():
             gather_frame(shards[b], layout, index, gathered[b], frames[b])
             gathered_ev[b] = torch.cuda.Event()
             gathered_ev[b].record(comm)
+        return b
 
     for i in range(a.warmup):
         step(i)
@@ -236,33 +346,72 @@ def main():
     st = ds.last_stats()
     phases = ds.last_timings()  # {phase: (ms over the K steps, launches)}
     dom = max(phases, key=lambda k: phases[k][0])
-    dom_ms = phases[dom][0] / a.steps  # per frame; one launch per frame at N=1 (one chunk)
+    dom_ms = phases[dom][0] / a.steps  # per frame
     dom_launches = phases[dom][1] / a.steps
     render_ms = sum(v[0] for v in phases.values()) / a.steps
 
-    t = torch.tensor([elapsed, dom_ms, render_ms], dtype=torch.float64, device=dev)
+    # ---- end to end (untimed above): render + gather + the float frame to host memory
+    # (what raytrace() returns, image4f) + the device tonemap of save_hdr_or_ldr's PNG
+    e2e_frames = max(1, min(a.steps, 3))
+    host_frame = torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True) if rank == 0 else None
+    ldr = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for i in range(e2e_frames):
+        b = step(a.steps + i)
+        if rank == 0:
+            if overlap:
+                stream.wait_event(gathered_ev[b])
+            yrt.tonemap_device(frames[b].data_ptr(), H * W, ldr.data_ptr(), stream=stream.cuda_stream)
+            host_frame.copy_(frames[b], non_blocking=True)
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    e2e_ms = (time.perf_counter() - t1) / e2e_frames * 1e3
+
+    t = torch.tensor([elapsed, dom_ms, render_ms, e2e_ms], dtype=torch.float64, device=dev)
     rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
-    elapsed, dom_ms, render_ms = float(t[0]), float(t[1]), float(t[2])
+    elapsed, dom_ms, render_ms, e2e_ms = (float(v) for v in t)
     total_rays, total_samples = float(rays[0]), float(rays[1])
-    alg_bytes = alg.get(dom)
 
     if rank == 0:
-        # per launch: algorithmic bytes of one frame's launch(es) / their mean duration
-        achieved = (alg_bytes / dom_launches) / (dom_ms / dom_launches / 1e3) / 1e9 if alg_bytes else None
+        spp = a.samples * a.samples
+        is_c4 = (a.scene, a.resolution, a.width, a.samples) == ("instance10000", 1080, 0, 8)
+        metric = BASELINE_METRIC if is_c4 else f"Mrays/sec + ms/frame, {a.scene} {W}×{H}×{spp}spp, {world} MI355X"
+        key = f"{a.scene}-{W}x{H}-s{a.samples}-n{world}-{a.algorithm}-{dom}"
+        kernel_ms = dom_ms / dom_launches
         traffic = None
-        tj = Path(a.traffic_json)
-        if tj.exists():
-            try:
-                tr = json.loads(tj.read_text())
-                key = f"{a.scene}-r{a.resolution}-s{a.samples}-n{world}-{a.algorithm}-{dom}"
-                traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        try:
+            tr = json.loads(Path(a.traffic_json).read_text())
+            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+        issue = issue_roofline(Path(a.issue_json), key, kernel_ms)
+        if issue:
+            bound, pipes, rec = issue
+            roof = {"bound": "issue", "pipe": bound, "achieved": pipes[bound]["achieved"],
+                    "peak": pipes[bound]["peak"], "unit": "G wave-instructions/s", "frac": pipes[bound]["frac"],
+                    "traffic": traffic, "kernel": PHASE_KERNEL.get(dom, dom), "kernel_ms": kernel_ms,
+                    "pipes": pipes, "counters": rec.get("source"),
+                    "hbm": {"bytes_per_launch": traffic,
+                            "achieved_GBs": traffic / (kernel_ms / 1e3) / 1e9 if traffic else None,
+                            "peak_GBs": HBM_PEAK_GBS,
+                            "frac": traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None},
+                    "note": ("SQ_INSTS_* per launch from the committed rocprofv3 counters of this exact "
+                             "configuration / live HIP-event launch time; peak at the 2.4 GHz max clock")}
+        else:
+            roof = {"bound": "issue", "achieved": None, "peak": None, "unit": "G wave-instructions/s",
+                    "frac": None, "traffic": traffic, "kernel": PHASE_KERNEL.get(dom, dom),
+                    "kernel_ms": kernel_ms,
+                    "note": f"no committed instruction counters for {key} (tools/gpu_issue_pmc.sh)"}
         line = {
-            "metric": "Mrays/sec + ms/frame, instance10000 1920x1080x64spp, 1/2/4/8 MI355X",
+            "metric": metric,
             "value": total_rays / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -273,25 +422,26 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "in/instance10000_pointlight scene (reference input, .yrtscene); deterministic camera samples",
+            "data": f"in/{a.scene} scene (reference input, .yrtscene); deterministic camera samples",
             "config": {"workload": f"{a.scene} {W}x{H} {a.samples}x{a.samples} spp, amb 0.1, one frame per step",
-                       "scene": a.scene, "width": W, "height": H, "spp": a.samples * a.samples,
-                       "parallelism": (f"image bands x{world} + RCCL all_gather" +
+                       "scene": a.scene, "width": W, "height": H, "spp": spp,
+                       "parallelism": (f"image bands x{world} + {backend_name} all_gather" +
                                        (" overlapped with the next frame" if overlap else "")) if world > 1
                        else "single GPU",
                        "rays_per_frame": total_rays / a.steps,
                        "camera_samples_per_frame": total_samples / a.steps,
                        "gpu_ms_per_frame": render_ms,
+                       "ms_per_frame_end_to_end": e2e_ms,
+                       "end_to_end": "render + gather + float frame to pinned host memory + device tonemap",
                        "phase_ms_per_frame": {k: v[0] / a.steps for k, v in phases.items()},
                        "camera_Msamples_per_s": total_samples / elapsed / 1e6,
                        "algorithm": a.algorithm},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                         "kernel": kernel_names.get(dom, dom), "kernel_ms": dom_ms / dom_launches,
-                         "algorithmic_bytes_per_launch": alg_bytes / dom_launches if alg_bytes else None},
+            "roofline": roof,
         }
         if world == 1 and a.cpu_seconds > 0:
-            line["cpu_baseline"] = cpu_baseline(scene_file, a.resolution, a.samples, a.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(scene_file, a.resolution, a.width, a.samples, a.cpu_seconds)
+            line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(scene_file, a.resolution, a.width, a.samples,
+                                                                    a.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -196,6 +196,33 @@ int yrt_last_timings(yrt_scene* ds, yrt_timings* timings);
 int yrt_tonemap(const float* rgba, int n, unsigned char* out, int mem, void* stream);
 /* save_hdr_or_ldr (src/image.cpp:81-88): .hdr -> RGBE, else PNG of the tonemap */
 int yrt_save_image(const char* path, const float* rgba, int w, int h);
+/* the same for a frame in `mem` space: with YRT_MEM_DEVICE the PNG's tonemap runs on the
+ * GPU (the stream's device) and only the RGBA8 image crosses PCIe; .hdr copies the floats */
+int yrt_save_image_mem(const char* path, const float* rgba, int w, int h, int mem, void* stream);
+
+/* ---- the GPUs of one node, one host process ----
+ * Replaces main()'s single raytrace() call (src/raytrace.cpp:282) for N devices: the
+ * scene is replicated on every device, device r renders the interleaved 8-row image
+ * bands r, r+n, r+2n, ..., and the float framebuffer is gathered to devices[0] over
+ * RCCL (grouped ncclSend/ncclRecv over xGMI) and reassembled in image order. A device
+ * listed twice uses plain device copies instead (a rehearsal on fewer GPUs). */
+typedef struct yrt_multi yrt_multi;
+enum { YRT_TRANSPORT_COPY = 0, YRT_TRANSPORT_RCCL = 1 };
+int yrt_multi_create(const yrt_host_scene* hs, const int* devices, int n, yrt_multi** out);
+void yrt_multi_free(yrt_multi* m);
+/* n devices and the gather transport (YRT_TRANSPORT_*) */
+int yrt_multi_info(const yrt_multi* m, int* n, int* transport);
+/* raytrace() of the whole frame (window/band fields of p must be defaults). out: W*H*4
+ * floats, host memory or device memory on devices[0]. Synchronous. */
+int yrt_multi_render(yrt_multi* m, const yrt_render_params* p, float* out, int mem);
+/* counters of the last yrt_multi_render summed over the devices */
+int yrt_multi_last_stats(yrt_multi* m, yrt_stats* stats);
+/* ms of the last yrt_multi_render on the root's stream: until every shard is rendered,
+ * then gather + reassembly */
+int yrt_multi_last_timings(const yrt_multi* m, float* render_ms, float* gather_ms);
+/* one-shot: create, render, free */
+int yrt_render_multi(const yrt_host_scene* hs, const int* devices, int n, const yrt_render_params* p, float* out,
+                     int mem);
 
 #ifdef __cplusplus
 }

@@ -81,16 +81,35 @@ inline void check(int status, const char* where) {
 // the reference's scene* (scene.h:136-155): host arrays + BVH, plus the device copies
 struct scene {
     yrt_host_scene* host = nullptr;
-    int device = 0;                          // GPU used by raytrace/intersect_*
+    int device = 0;                          // GPU used by raytrace/intersect_* (gpus == 1)
+    int gpus = 1;                            // raytrace on GPUs device..device+gpus-1 (yrt_multi)
     yrt_render_params params{};              // extras beyond the reference's signature
     mutable std::map<int, yrt_scene*> dev;   // uploaded lazily, one per device
+    mutable yrt_multi* multi = nullptr;      // the replicas for gpus > 1, made lazily
+    mutable int multi_key[2] = {-1, 0};      // {device, gpus} of `multi`
 
     scene() { yrt_render_params_default(&params); }
     scene(const scene&) = delete;
     scene& operator=(const scene&) = delete;
     ~scene() {
-        for (auto& kv : dev) yrt_scene_free(kv.second);
+        release();
         if (host) yrt_host_scene_free(host);
+    }
+    void release() const {
+        for (auto& kv : dev) yrt_scene_free(kv.second);
+        dev.clear();
+        if (multi) yrt_multi_free(multi);
+        multi = nullptr;
+    }
+    yrt_multi* on_devices() const {
+        if (multi && multi_key[0] == device && multi_key[1] == gpus) return multi;
+        if (multi) yrt_multi_free(multi);
+        multi = nullptr;
+        std::vector<int> ids(gpus);
+        for (int k = 0; k < gpus; k++) ids[k] = device + k;
+        check(yrt_multi_create(host, ids.data(), gpus, &multi), "yrt_multi_create");
+        multi_key[0] = device, multi_key[1] = gpus;
+        return multi;
     }
     yrt_scene* on_device() const {
         auto it = dev.find(device);
@@ -111,12 +130,12 @@ inline std::unique_ptr<scene> load_scene(const std::string& filename) {
 
 // build_bvh (src/scene.cpp:554-565)
 inline void build_bvh(const std::unique_ptr<scene>& scn, bool equal_num) {
-    for (auto& kv : scn->dev) yrt_scene_free(kv.second);
-    scn->dev.clear();
+    scn->release();
     check(yrt_host_scene_build_bvh(scn->host, equal_num ? 1 : 0), "build_bvh");
 }
 
-// raytrace (src/raytrace.cpp:213-254): resolution = vertical size, samples per axis
+// raytrace (src/raytrace.cpp:213-254): resolution = vertical size, samples per axis.
+// With scn->gpus > 1 the frame is split over that many GPUs (8-row bands, RCCL gather).
 inline image4f raytrace(const std::unique_ptr<scene>& scn, const vec3f& amb, int resolution, int samples) {
     yrt_scene* ds = scn->on_device();
     yrt_render_params p = scn->params;
@@ -126,8 +145,21 @@ inline image4f raytrace(const std::unique_ptr<scene>& scn, const vec3f& amb, int
     int w = 0, h = 0;
     check(yrt_image_size(ds, &p, &w, &h), "raytrace");
     image4f img(w, h);
-    check(yrt_render(ds, &p, &img.pixels[0].x, YRT_MEM_HOST, nullptr), "raytrace");
+    if (scn->gpus > 1)
+        check(yrt_multi_render(scn->on_devices(), &p, &img.pixels[0].x, YRT_MEM_HOST), "raytrace");
+    else
+        check(yrt_render(ds, &p, &img.pixels[0].x, YRT_MEM_HOST, nullptr), "raytrace");
     return img;
+}
+
+// counters of the last raytrace (summed over the GPUs when gpus > 1)
+inline yrt_stats last_stats(const std::unique_ptr<scene>& scn) {
+    yrt_stats st{};
+    if (scn->gpus > 1 && scn->multi)
+        check(yrt_multi_last_stats(scn->multi, &st), "last_stats");
+    else
+        check(yrt_last_stats(scn->on_device(), &st), "last_stats");
+    return st;
 }
 
 // batch intersect_first (scene.cpp:483-488)

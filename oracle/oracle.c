@@ -35,6 +35,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 typedef struct { float x, y; } v2;
 typedef struct { float x, y, z; } v3;
@@ -621,6 +624,18 @@ int oracle_image_size(void* vs, int cami, int resolution, int* w, int* h) {
     *w = (int)roundf(s->cams[cami].aspect * resolution);
     *h = resolution;
     return 0;
+}
+
+/* threads of the OpenMP loops below (row-parallel render, ray-parallel trace); returns
+ * the count in effect. The reference is single-threaded: 1 is its equivalent. */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }
 
 /* raytrace() (raytrace.cpp:213-254) for image rows rows[0..nrows) and columns

@@ -8,11 +8,16 @@
 //   yrt_host_scene* yrt_from_reference_scene(const scene*)     scene.h:26-155 -> yrt.h builder
 //   image4f raytrace_gpu(const scene*, const vec3f&, int, int) same signature as raytrace(),
 //                                                               src/raytrace.cpp:213
-//   void raytrace_gpu_release(const scene*)                     drop the scene's device copy
+//   image4f raytrace_gpu(const scene*, const vec3f&, int, int, int gpus)
+//                                                               the same on GPUs 0..gpus-1 of the node
+//                                                               (yrt_multi: bands + RCCL gather)
+//   void raytrace_gpu_release(const scene*)                     drop the scene's device copies
 #include "scene.h"
 #include "yrt.h"
 
+#include <cmath>
 #include <cstdio>
+#include <vector>
 #include <cstring>
 #include <unordered_map>
 
@@ -86,13 +91,21 @@ yrt_host_scene* yrt_from_reference_scene(const scene* scn) {
 
 // device copies, one per scene, made on first use and kept until released
 static std::unordered_map<const scene*, yrt_scene*> resident;
+// multi-GPU replicas, one per scene (and GPU count)
+static std::unordered_map<const scene*, std::pair<int, yrt_multi*>> resident_multi;
 
-// drop the device copy of `scn` (call before deleting or editing the scene)
+// drop the device copies of `scn` (call before deleting or editing the scene)
 void raytrace_gpu_release(const scene* scn) {
     auto it = resident.find(scn);
-    if (it == resident.end()) return;
-    yrt_scene_free(it->second);
-    resident.erase(it);
+    if (it != resident.end()) {
+        yrt_scene_free(it->second);
+        resident.erase(it);
+    }
+    auto im = resident_multi.find(scn);
+    if (im != resident_multi.end()) {
+        yrt_multi_free(im->second.second);
+        resident_multi.erase(im);
+    }
 }
 
 // raytrace() (src/raytrace.cpp:213) on the GPU: same arguments, same image4f. The
@@ -122,6 +135,38 @@ image4f raytrace_gpu(const scene* scn, const vec3f& amb, int resolution, int sam
     return img;
 }
 
+// raytrace() on GPUs 0..gpus-1 of the node: the scene replicated on each, interleaved
+// 8-row bands per GPU, the framebuffer gathered over RCCL (yrt.h yrt_multi_*)
+image4f raytrace_gpu(const scene* scn, const vec3f& amb, int resolution, int samples, int gpus) {
+    if (gpus <= 1) return raytrace_gpu(scn, amb, resolution, samples);
+    auto& slot = resident_multi[scn];
+    if (!slot.second || slot.first != gpus) {
+        if (slot.second) yrt_multi_free(slot.second);
+        slot.second = nullptr;
+        yrt_host_scene* hs = yrt_from_reference_scene(scn);
+        std::vector<int> devices(gpus);
+        for (int k = 0; k < gpus; k++) devices[k] = k;
+        if (!hs || yrt_multi_create(hs, devices.data(), gpus, &slot.second) != YRT_OK) {
+            fprintf(stderr, "raytrace_gpu: %s\n", yrt_last_error());
+            exit(1);
+        }
+        slot.first = gpus;
+        yrt_host_scene_free(hs);
+    }
+    yrt_render_params p;
+    yrt_render_params_default(&p);
+    p.ambient[0] = amb.x, p.ambient[1] = amb.y, p.ambient[2] = amb.z;
+    p.resolution = resolution;
+    p.samples = samples;
+    const int w = (int)round(scn->cameras.front()->aspect * resolution), h = resolution;  // raytrace.cpp:215-216
+    image4f img(w, h);
+    if (yrt_multi_render(slot.second, &p, &img.pixels[0].x, YRT_MEM_HOST) != YRT_OK) {
+        fprintf(stderr, "raytrace_gpu: %s\n", yrt_last_error());
+        exit(1);
+    }
+    return img;
+}
+
 // ---- ctypes entry points for tests/test_integration.py ----
 extern "C" {
 
@@ -145,6 +190,12 @@ void ref_int_release(void* refscn) { raytrace_gpu_release((const scene*)refscn);
 
 int ref_int_render(void* refscn, float amb, int resolution, int samples, float* out) {
     image4f img = raytrace_gpu((const scene*)refscn, {amb, amb, amb}, resolution, samples);
+    memcpy(out, img.pixels.data(), img.pixels.size() * sizeof(vec4f));
+    return 0;
+}
+
+int ref_int_render_gpus(void* refscn, float amb, int resolution, int samples, int gpus, float* out) {
+    image4f img = raytrace_gpu((const scene*)refscn, {amb, amb, amb}, resolution, samples, gpus);
     memcpy(out, img.pixels.data(), img.pixels.size() * sizeof(vec4f));
     return 0;
 }

@@ -1,14 +1,19 @@
-"""Summarise rocprofv3 counter CSVs into per-kernel HBM traffic per launch.
+"""Summarise rocprofv3 counter CSVs into the two files bench.py reads.
 
-    python tools/pmc_summary.py --key instance10000-r1080-s8-n1-wavefront \
-        --fetch gpurun_out/p3/p3_counter_collection.csv \
-        --write gpurun_out/p4/p4_counter_collection.csv \
-        [--kernel-trace gpurun_out/ks/ks_kernel_stats.csv] > profiles/pmc_traffic.json
+    python tools/pmc_summary.py --key instance10000-1920x1080-s8-n1-wavefront \
+        --csv gpurun_out/T/p*/p*_counter_collection.csv --source profiles/r2/T \
+        --traffic profiles/pmc_traffic.json --issue profiles/issue_counters.json
 
-HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: on gfx950
-FETCH_SIZE reports half the bytes of wide coalesced streaming reads (16 B/lane), and
-WRITE_SIZE is exact for 16-B stores (MI355X_MICROARCH.md, HBM section); both come
-from separate --pmc passes. Only the un-instrumented (COUNT=false, first template argument) kernels are kept.
+Per timed kernel (COUNT=false, first template argument) and per launch:
+* traffic: HBM bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024. On gfx950 FETCH_SIZE
+  reports half the bytes of wide coalesced streaming reads (16 B/lane) and WRITE_SIZE is
+  exact for 16-B stores (MI355X_MICROARCH.md, HBM section); separate --pmc passes.
+* issue: the SQ_* / GRBM_* / SQC_* counters as collected (chip totals per launch), plus
+  derived rates: clock cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs);
+  SALU busy = SQ_INSTS_SALU / (256 CUs x cycles) (one scalar unit per CU, one issue per
+  clock); VALU busy = SQ_INSTS_VALU / (256 x 4 SIMDs x cycles / 2) (a wave64 VALU
+  instruction takes two clocks on a SIMD-32); scalar-cache hit rate.
+Entries are merged into the existing files (same key = replaced).
 """
 from __future__ import annotations
 
@@ -17,6 +22,7 @@ import collections
 import csv
 import json
 import re
+from pathlib import Path
 
 PHASE_OF = {"k_primary": "primary", "k_shadow": "shadow", "k_shade": "shade", "k_bounce": "bounce",
             "k_fold_children": "fold", "k_accumulate": "accumulate", "render_kernel": "megakernel"}
@@ -28,42 +34,62 @@ def short(name: str) -> str:
     return (m.group(1) + (m.group(2) or "")) if m else name[:40]
 
 
-def per_launch(path: str, counter: str) -> dict:
+def per_launch(paths) -> dict:
+    """{kernel: {counter: mean value per dispatch}}"""
     vals = collections.defaultdict(float)
     launches = collections.defaultdict(set)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        k = short(r["Kernel_Name"])
-        if re.match(r"\w+<true", k):  # COUNT=true: the instrumented twin
-            continue
-        vals[k] += float(r["Counter_Value"])
-        launches[k].add(r["Dispatch_Id"])
-    return {k: vals[k] / max(1, len(launches[k])) for k in vals}
+    for path in paths:
+        for r in csv.DictReader(open(path)):
+            k = short(r["Kernel_Name"])
+            if re.match(r"\w+<true", k):  # COUNT=true: the instrumented twin
+                continue
+            vals[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+            launches[(k, r["Counter_Name"])].add((path, r["Dispatch_Id"]))
+    out = collections.defaultdict(dict)
+    for (k, c), v in vals.items():
+        out[k][c] = v / max(1, len(launches[(k, c)]))
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--key", required=True)
-    ap.add_argument("--fetch", required=True)
-    ap.add_argument("--write", required=True)
-    ap.add_argument("--merge", help="existing json to extend")
+    ap.add_argument("--key", required=True, help="{scene}-{W}x{H}-s{spp axis}-n{ranks}-{algorithm}")
+    ap.add_argument("--csv", nargs="+", required=True)
+    ap.add_argument("--source", default="", help="where the CSVs are committed")
+    ap.add_argument("--traffic", default="profiles/pmc_traffic.json")
+    ap.add_argument("--issue", default="profiles/issue_counters.json")
     a = ap.parse_args()
-    fetch = per_launch(a.fetch, "FETCH_SIZE")
-    write = per_launch(a.write, "WRITE_SIZE")
-    out = json.load(open(a.merge)) if a.merge else {}
-    for k in sorted(set(fetch) | set(write)):
-        base = k.split("<")[0]
-        phase = PHASE_OF.get(base)
+    data = per_launch(a.csv)
+    traffic = json.loads(Path(a.traffic).read_text()) if Path(a.traffic).exists() else {}
+    issue = json.loads(Path(a.issue).read_text()) if Path(a.issue).exists() else {}
+    for k, c in sorted(data.items()):
+        phase = PHASE_OF.get(k.split("<")[0])
         if not phase:
             continue
-        f, w = fetch.get(k, 0.0), write.get(k, 0.0)
-        out[f"{a.key}-{phase}"] = {
-            "kernel": k, "fetch_size_kb": f, "write_size_kb": w,
-            "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
-            "note": "2*FETCH_SIZE (gfx950 half-count on 16B/lane streams) + WRITE_SIZE, KB->B",
-        }
-    print(json.dumps(out, indent=1))
+        key = f"{a.key}-{phase}"
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            f, w = c["FETCH_SIZE"], c["WRITE_SIZE"]
+            traffic[key] = {"kernel": k, "fetch_size_kb": f, "write_size_kb": w,
+                            "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024, "source": a.source,
+                            "note": "2*FETCH_SIZE (gfx950 half-count on 16B/lane streams) + WRITE_SIZE, KB->B"}
+        rec = {n: v for n, v in c.items() if n.startswith(("SQ_", "SQC_", "GRBM_"))}
+        if "SQ_INSTS_SALU" in rec and "SQ_INSTS_VALU" in rec:
+            rec = {"kernel": k, "source": a.source, **rec}
+            cyc = rec.get("GRBM_GUI_ACTIVE", 0) / 8
+            if cyc:
+                rec["cycles"] = cyc
+                rec["salu_busy"] = rec["SQ_INSTS_SALU"] / (256 * cyc)
+                rec["valu_busy"] = rec["SQ_INSTS_VALU"] * 2 / (256 * 4 * cyc)
+            if rec.get("SQ_WAVES"):
+                rec["salu_per_wave"] = rec["SQ_INSTS_SALU"] / rec["SQ_WAVES"]
+                rec["valu_per_wave"] = rec["SQ_INSTS_VALU"] / rec["SQ_WAVES"]
+            h, m = rec.get("SQC_DCACHE_HITS"), rec.get("SQC_DCACHE_MISSES")
+            if h is not None and m is not None and h + m:
+                rec["sqc_dcache_hit_rate"] = h / (h + m)
+            issue[key] = rec
+    Path(a.traffic).write_text(json.dumps(traffic, indent=1, sort_keys=True) + "\n")
+    Path(a.issue).write_text(json.dumps(issue, indent=1, sort_keys=True) + "\n")
+    print(json.dumps({k: v for k, v in issue.items() if k.startswith(a.key)}, indent=1))
 
 
 if __name__ == "__main__":

@@ -209,6 +209,48 @@ class DeviceScene:
         return {name: int(getattr(s, name)) for name, _ in Stats._fields_}
 
 
+class MultiScene:
+    """A scene replicated on several GPUs of this node (yrt_multi*): raytrace() of a
+    whole frame split into interleaved 8-row bands, gathered to devices[0] over RCCL
+    (or plain copies when a device is listed twice -- a rehearsal on one GPU)."""
+
+    def __init__(self, scene: "Scene", devices: Sequence[int]):
+        ids = (C.c_int * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        check(N.lib.yrt_multi_create(scene.handle, ids, len(devices), C.byref(h)), "yrt_multi_create")
+        self._h = h
+        self.devices = tuple(int(d) for d in devices)
+        n, tr = C.c_int(), C.c_int()
+        check(N.lib.yrt_multi_info(self._h, C.byref(n), C.byref(tr)), "yrt_multi_info")
+        self.transport = "rccl" if tr.value == N.YRT_TRANSPORT_RCCL else "copy"
+
+    def close(self):
+        if self._h:
+            N.lib.yrt_multi_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render_into(self, params: RenderParams, out_ptr: int, device_memory: bool = False) -> None:
+        """raytrace() of the whole frame into a host buffer, or a device buffer on devices[0]"""
+        mem = N.YRT_MEM_DEVICE if device_memory else N.YRT_MEM_HOST
+        check(N.lib.yrt_multi_render(self._h, C.byref(params), C.c_void_p(out_ptr), mem), "yrt_multi_render")
+
+    def last_stats(self) -> dict:
+        s = Stats()
+        check(N.lib.yrt_multi_last_stats(self._h, C.byref(s)), "yrt_multi_last_stats")
+        return {name: int(getattr(s, name)) for name, _ in Stats._fields_}
+
+    def last_timings(self) -> dict:
+        r, g = C.c_float(), C.c_float()
+        check(N.lib.yrt_multi_last_timings(self._h, C.byref(r), C.byref(g)), "yrt_multi_last_timings")
+        return {"render_ms": r.value, "gather_ms": g.value}
+
+
 def device_count() -> int:
     n = C.c_int(0)
     N.lib.yrt_device_count(C.byref(n))
@@ -257,11 +299,27 @@ def _device_scene(scn, device: int = 0) -> DeviceScene:
 
 def raytrace(scn, amb: Sequence[float] = (0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1,
              *, width: int = 0, max_depth: int = 16, camera: int = 0, window=None,
-             count_work: bool = False, return_stats: bool = False, algorithm: str = "wavefront"):
+             count_work: bool = False, return_stats: bool = False, algorithm: str = "wavefront",
+             devices: Optional[Sequence[int]] = None):
     """raytrace (src/raytrace.cpp:213): RGBA float32 image (H, W, 4), row-major.
 
     `samples` is per axis (s*s samples per pixel), `resolution` the vertical size.
-    `window` = (x0, y0, w, h) renders a sub-rectangle only."""
+    `window` = (x0, y0, w, h) renders a sub-rectangle only. `devices` (a Scene, whole
+    frames) splits the frame over those GPUs (MultiScene)."""
+    if devices is not None:
+        if window is not None or isinstance(scn, DeviceScene):
+            raise ValueError("devices= renders whole frames of a host Scene")
+        ms = MultiScene(scn, devices)
+        try:
+            p = render_params(amb, resolution, samples, width=width, max_depth=max_depth, camera=camera,
+                              count_work=count_work, algorithm=algorithm)
+            W, H = scn.upload(devices[0]).image_size(p)
+            img = np.zeros((H, W, 4), np.float32)
+            ms.render_into(p, img.ctypes.data)
+            stats = ms.last_stats()
+        finally:
+            ms.close()
+        return (img, stats) if return_stats else img
     ds = _device_scene(scn)
     p = render_params(amb, resolution, samples, width=width, max_depth=max_depth, camera=camera,
                       window=window, count_work=count_work, algorithm=algorithm)
@@ -314,6 +372,18 @@ def tonemap(img: np.ndarray) -> np.ndarray:
     out = np.zeros(a.shape, np.uint8)
     check(N.lib.yrt_tonemap(a.ctypes.data, a.size // 4, out.ctypes.data, N.YRT_MEM_HOST, None), "tonemap")
     return out
+
+
+def save_image_device(filename: str, ptr: int, width: int, height: int, stream: Optional[int] = None) -> None:
+    """save_hdr_or_ldr of a frame in device memory: the PNG tonemap runs on the GPU"""
+    check(N.lib.yrt_save_image_mem(str(filename).encode(), C.c_void_p(ptr), int(width), int(height),
+                                   N.YRT_MEM_DEVICE, C.c_void_p(stream or 0)), "save_image_device")
+
+
+def tonemap_device(rgba_ptr: int, n: int, out_ptr: int, stream: Optional[int] = None) -> None:
+    """tonemap (src/image.cpp:55) of n RGBA f32 pixels in device memory into RGBA8 (device)"""
+    check(N.lib.yrt_tonemap(C.c_void_p(rgba_ptr), int(n), C.c_void_p(out_ptr), N.YRT_MEM_DEVICE,
+                            C.c_void_p(stream or 0)), "tonemap_device")
 
 
 def save_hdr_or_ldr(filename: str, img: np.ndarray) -> None:

@@ -22,6 +22,8 @@ lib = C.CDLL(str(LIB_PATH))
 YRT_OK = 0
 YRT_MEM_HOST = 0
 YRT_MEM_DEVICE = 1
+YRT_TRANSPORT_COPY = 0
+YRT_TRANSPORT_RCCL = 1
 
 
 class RenderParams(C.Structure):
@@ -105,6 +107,14 @@ _sig = {
     "yrt_last_timings": (C.c_int, [_vp, C.POINTER(Timings)]),
     "yrt_tonemap": (C.c_int, [_vp, C.c_int, _vp, C.c_int, _vp]),
     "yrt_save_image": (C.c_int, [C.c_char_p, _vp, C.c_int, C.c_int]),
+    "yrt_save_image_mem": (C.c_int, [C.c_char_p, _vp, C.c_int, C.c_int, C.c_int, _vp]),
+    "yrt_multi_create": (C.c_int, [_vp, _ip, C.c_int, C.POINTER(_vp)]),
+    "yrt_multi_free": (None, [_vp]),
+    "yrt_multi_info": (C.c_int, [_vp, _ip, _ip]),
+    "yrt_multi_render": (C.c_int, [_vp, C.POINTER(RenderParams), _vp, C.c_int]),
+    "yrt_multi_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
+    "yrt_multi_last_timings": (C.c_int, [_vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "yrt_render_multi": (C.c_int, [_vp, _ip, C.c_int, C.POINTER(RenderParams), _vp, C.c_int]),
 }
 EXPORTS = tuple(_sig)
 

@@ -2,8 +2,8 @@
 
 hipcc drives everything (no cmake): host C++ and the gfx950 kernels are compiled
 with -ffp-contract=off so that no a*b+c is fused anywhere on the hot path (the
-reference's x86-64 build has no FMA). Objects are rebuilt only when
-a source or header is newer.
+reference's x86-64 build has no FMA). Objects are rebuilt when a
+source or header is newer or the compile command (flags, -D knobs) changed.
 
     python yocto_raytracing_amd/build.py            # library + CLI
     python yocto_raytracing_amd/build.py --oracle   # + oracle/liboracle.so (+ oracle/_ref if present)
@@ -27,12 +27,13 @@ CLANGXX = os.environ.get("YRT_CXX", "/opt/rocm/lib/llvm/bin/clang++")
 ARCH = os.environ.get("YRT_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["obj_loader.cpp", "png.cpp", "scene_io.cpp", "bvh_build.cpp",
-           "device_scene.cpp", "capi.cpp", "render.hip", "wavefront.hip"]
+           "device_scene.cpp", "capi.cpp", "multi.cpp", "render.hip", "wavefront.hip"]
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           f"-I{CSRC}", f"-I{ROOT / 'include'}"]
 
 
 HOST_DEFS = ["-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+LINK_LIBS = ["-lz", "-ldl", "-lpthread"]
 # device code: leave wave-uniform regions unstructurized. Every branch of the BVH walks
 # is on an SGPR value; structurizing them adds flow variables and exec-mask juggling
 # (SALU) to every traversal step (A/B at c4: primary -2 %, shadow -4 %).
@@ -43,11 +44,21 @@ def _headers():
     return list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h*"))
 
 
-def _stale(out: Path, deps) -> bool:
+def _stale(out: Path, deps, cmd=None) -> bool:
+    """out is missing, older than a dependency, or was built by a different command
+    (flags, -D knobs, compiler): the command is kept in a stamp file next to it"""
     if not out.exists():
         return True
+    if cmd is not None:
+        stamp = out.with_name(out.name + ".cmd")
+        if not stamp.exists() or stamp.read_text() != " ".join(map(str, cmd)):
+            return True
     t = out.stat().st_mtime
     return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _stamp(out: Path, cmd) -> None:
+    out.with_name(out.name + ".cmd").write_text(" ".join(map(str, cmd)))
 
 
 def _run(cmd):
@@ -66,22 +77,32 @@ def build_library(verbose: bool = False) -> Path:
         s = CSRC / src
         o = BUILD / (s.stem + ".o")
         objs.append(o)
-        if _stale(o, [s, *hdrs]):
-            if src.endswith(".hip"):
-                cmd = [HIPCC, *COMMON, *DEVICE_FLAGS, f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)]
-            else:  # host-only C++: same clang, no offload
-                cmd = [CLANGXX, *COMMON, *HOST_DEFS, "-c", str(s), "-o", str(o)]
-            jobs.append(cmd)
+        if src.endswith(".hip"):
+            cmd = [HIPCC, *COMMON, *DEVICE_FLAGS, f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)]
+        else:  # host-only C++: same clang, no offload
+            cmd = [CLANGXX, *COMMON, *HOST_DEFS, "-c", str(s), "-o", str(o)]
+        if _stale(o, [s, *hdrs], cmd):
+            jobs.append((o, cmd))
+
+    def job(item):
+        o, cmd = item
+        r = _run(cmd)
+        _stamp(o, cmd)
+        return r
+
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        for r in ex.map(_run, jobs):
+        for r in ex.map(job, jobs):
             if verbose:
                 print(r.stderr, end="")
-    if _stale(LIB, objs):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(LIB), *map(str, objs), "-lz"])
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(LIB), *map(str, objs), *LINK_LIBS]
+    if _stale(LIB, objs, link):
+        _run(link)
+        _stamp(LIB, link)
     cli_src = CSRC / "cli.cpp"
-    if cli_src.exists() and _stale(CLI, [cli_src, LIB, *hdrs]):
-        _run([CLANGXX, *COMMON, *HOST_DEFS, str(cli_src), "-o", str(CLI),
-              f"-L{PKG}", "-lyrt", "-Wl,-rpath,$ORIGIN"])
+    cli = [CLANGXX, *COMMON, *HOST_DEFS, str(cli_src), "-o", str(CLI), f"-L{PKG}", "-lyrt", "-Wl,-rpath,$ORIGIN"]
+    if cli_src.exists() and _stale(CLI, [cli_src, LIB, *hdrs], cli):
+        _run(cli)
+        _stamp(CLI, cli)
     return LIB
 
 

@@ -8,6 +8,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/yrt.h"
 #include "yrt_render.h"
@@ -29,22 +30,26 @@ namespace {
 
 thread_local std::string g_last_error;
 
-struct hip_failure : std::runtime_error {
-    using std::runtime_error::runtime_error;
-};
-
 void hip_check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw hip_failure(std::string(what) + ": " + hipGetErrorString(e));
+    if (e == hipErrorOutOfMemory) throw yrt::device_oom(std::string(what) + ": " + hipGetErrorString(e));
+    if (e != hipSuccess) throw yrt::device_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// exception type -> status code (yrt_scene.h lists the mapping); the message is kept
 template <class F>
 int guarded(F&& f) {
     try {
         g_last_error.clear();
         return f();
-    } catch (const hip_failure& e) {
+    } catch (const yrt::device_oom& e) {
+        g_last_error = e.what();
+        return YRT_ERR_OOM;
+    } catch (const yrt::device_error& e) {
         g_last_error = e.what();
         return YRT_ERR_HIP;
+    } catch (const yrt::unsupported_error& e) {
+        g_last_error = e.what();
+        return YRT_ERR_UNSUPPORTED;
     } catch (const std::bad_alloc&) {
         g_last_error = "out of memory";
         return YRT_ERR_OOM;
@@ -53,12 +58,6 @@ int guarded(F&& f) {
         return YRT_ERR_INVALID_ARG;
     } catch (const std::runtime_error& e) {
         g_last_error = e.what();
-        std::string m = e.what();
-        if (m.find("unsupported") != std::string::npos || m.find("too deep") != std::string::npos ||
-            m.find("not supported") != std::string::npos || m.find("mixes") != std::string::npos)
-            return YRT_ERR_UNSUPPORTED;
-        if (m.find("hipMalloc") != std::string::npos) return YRT_ERR_OOM;
-        if (m.find("hip") == 0) return YRT_ERR_HIP;
         return YRT_ERR_IO;
     } catch (...) {
         g_last_error = "internal error";
@@ -104,6 +103,8 @@ resolved_window resolve(const yrt::device_scene& ds, const yrt_render_params& p)
 }
 
 }  // namespace
+
+void yrt::set_last_error(const std::string& msg) { g_last_error = msg; }
 
 namespace {
 yrt::frame3f frame_of(const float* f) {
@@ -552,6 +553,34 @@ int yrt_save_image(const char* path, const float* rgba, int w, int h) {
     if (!path || !rgba || w <= 0 || h <= 0) return YRT_ERR_INVALID_ARG;
     return guarded([&] {
         yrt::save_hdr_or_ldr(path, rgba, w, h);
+        return YRT_OK;
+    });
+}
+
+int yrt_save_image_mem(const char* path, const float* rgba, int w, int h, int mem, void* stream) {
+    if (mem != YRT_MEM_DEVICE) return yrt_save_image(path, rgba, w, h);
+    if (!path || !rgba || w <= 0 || h <= 0) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        const std::string p = path;
+        const size_t n = (size_t)w * h;
+        hipStream_t st = (hipStream_t)stream;
+        if (p.size() >= 4 && p.substr(p.size() - 4) == ".hdr") {
+            std::vector<float> px(n * 4);
+            hip_check(hipMemcpyAsync(px.data(), rgba, n * 16, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+            hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+            yrt::save_hdr_or_ldr(p, px.data(), w, h);
+            return YRT_OK;
+        }
+        // tonemap on the GPU, then only the 8-bit image crosses PCIe
+        unsigned char* d8 = nullptr;
+        hip_check(hipMalloc(&d8, n * 4), "hipMalloc(tonemap)");
+        std::vector<unsigned char> ldr(n * 4);
+        hipError_t e = yrt::launch_tonemap(rgba, (int)n, d8, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(ldr.data(), d8, n * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipFree(d8);
+        hip_check(e, "device tonemap");
+        yrt::save_ldr_png(p, ldr.data(), w, h);
         return YRT_OK;
     });
 }

@@ -25,6 +25,7 @@ namespace {
             "  -a, --ambient F      ambient color [0.1]\n"
             "  -o, --output FILE    output image (.png tonemapped, .hdr float) [out.png]\n"
             "  --device N           GPU index [0]\n"
+            "  --gpus N             split the frame over N GPUs from --device on [1]\n"
             "  --width N            explicit width (default round(aspect * resolution))\n"
             "  --max-depth N        cap on reflection depth [16]\n"
             "  --algorithm NAME     wavefront | megakernel | wavefront_lane [wavefront]\n"
@@ -42,7 +43,7 @@ int parse_int(const char* s, const char* opt) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    int resolution = 720, samples = 1, device = 0, width = 0, max_depth = 16, algorithm = YRT_ALGO_WAVEFRONT;
+    int resolution = 720, samples = 1, device = 0, gpus = 1, width = 0, max_depth = 16, algorithm = YRT_ALGO_WAVEFRONT;
     float amb = 0.1f;
     bool timing = false;
     std::string out = "out.png", scenein;
@@ -57,6 +58,7 @@ int main(int argc, char** argv) {
         else if (a == "-a" || a == "--ambient") amb = strtof(val(), nullptr);
         else if (a == "-o" || a == "--output") out = val();
         else if (a == "--device") device = parse_int(val(), "--device");
+        else if (a == "--gpus") gpus = parse_int(val(), "--gpus");
         else if (a == "--width") width = parse_int(val(), "--width");
         else if (a == "--max-depth") max_depth = parse_int(val(), "--max-depth");
         else if (a == "--algorithm") {
@@ -72,12 +74,14 @@ int main(int argc, char** argv) {
         else usage("too many arguments");
     }
     if (scenein.empty()) scenein = "scene.obj";  // the reference's default positional value
+    if (gpus < 1) usage("--gpus must be >= 1");
     try {
         printf("loading scene %s\n", scenein.c_str());
         auto scn = yrt_cpp::load_scene(scenein);
         printf("creating bvh\n");
         yrt_cpp::build_bvh(scn, false);
         scn->device = device;
+        scn->gpus = gpus;
         scn->params.width = width;
         scn->params.max_depth = max_depth;
         scn->params.algorithm = algorithm;
@@ -87,11 +91,10 @@ int main(int argc, char** argv) {
         auto hdr = yrt_cpp::raytrace(scn, {amb, amb, amb}, resolution, samples);
         auto t1 = std::chrono::steady_clock::now();
         if (timing) {
-            yrt_stats st{};
-            yrt_last_stats(scn->on_device(), &st);
+            const yrt_stats st = yrt_cpp::last_stats(scn);
             double s = std::chrono::duration<double>(t1 - t0).count();
-            printf("render %dx%d x %d spp: %.3f ms (incl. copy to host), %llu rays, %.1f Mrays/s\n", hdr.width,
-                   hdr.height, samples * samples, s * 1e3, st.rays, st.rays / s / 1e6);
+            printf("render %dx%d x %d spp on %d GPU(s): %.3f ms (incl. copy to host), %llu rays, %.1f Mrays/s\n",
+                   hdr.width, hdr.height, samples * samples, gpus, s * 1e3, st.rays, st.rays / s / 1e6);
         }
         printf("saving image %s\n", out.c_str());
         yrt_cpp::save_hdr_or_ldr(out, hdr);

@@ -37,7 +37,8 @@ f4 node_hi(const bvh_node& n) {
 }
 
 void check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+    if (e == hipErrorOutOfMemory) throw device_oom(std::string(what) + ": " + hipGetErrorString(e));
+    if (e != hipSuccess) throw device_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
 struct arena_builder {
@@ -243,7 +244,7 @@ struct wide_builder {
             if (s.isleaf) {
                 const uint32_t first = s.start + leaf_base;
                 if (first > wide_index_mask || s.count > 7)
-                    throw std::runtime_error("scene too large for the wide any-hit records");
+                    throw unsupported_error("scene too large for the wide any-hit records");
                 word[k] = wide_leaf | ((uint32_t)s.count << wide_count_shift) | first;
             } else {
                 inner[k] = true;
@@ -252,7 +253,7 @@ struct wide_builder {
         for (int k = 0; k < 4; k++)
             if (inner[k]) {
                 const size_t off = (size_t)emit(t, slots[k], leaf_base, depth + 1) * wide_record_bytes;
-                if (off > wide_index_mask) throw std::runtime_error("scene too large for the wide any-hit records");
+                if (off > wide_index_mask) throw unsupported_error("scene too large for the wide any-hit records");
                 word[k] = (uint32_t)off;
             }
         for (int a = 0; a < 6; a++) out[(size_t)me * 8 + a] = {v[a][0], v[a][1], v[a][2], v[a][3]};
@@ -287,7 +288,7 @@ dev_camera make_dev_camera(const camera& c) {
 }
 
 device_scene* device_scene_create(const scene& scn, int device) {
-    if (!scn.has_bvh) throw std::runtime_error("scene has no BVH (call build_bvh first)");
+    if (!scn.has_bvh) throw std::invalid_argument("scene has no BVH (call build_bvh first)");
     if (scn.cameras.empty()) throw std::runtime_error("scene has no camera");
     if (scn.instances.empty()) throw std::runtime_error("scene has no instances");
 
@@ -298,9 +299,9 @@ device_scene* device_scene_create(const scene& scn, int device) {
             if (!n.isleaf && n.count != 2) return false;
         return !t.nodes.empty();
     };
-    if (!binary(scn.bvh)) throw std::runtime_error("instance BVH is not binary (unsupported)");
+    if (!binary(scn.bvh)) throw unsupported_error("instance BVH is not binary (unsupported)");
     for (auto& s : scn.shapes)
-        if (!binary(s.bvh)) throw std::runtime_error("shape BVH of " + s.name + " is not binary (unsupported)");
+        if (!binary(s.bvh)) throw unsupported_error("shape BVH of " + s.name + " is not binary (unsupported)");
 
     auto ds = new device_scene();
     ds->device = device;
@@ -310,7 +311,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     if (ds->top_depth + ds->shape_depth > traversal_stack_cap) {
         int td = ds->top_depth, sd = ds->shape_depth;
         delete ds;
-        throw std::runtime_error("BVH too deep for the kernel stacks (instance " + std::to_string(td) +
+        throw unsupported_error("BVH too deep for the kernel stacks (instance " + std::to_string(td) +
                                  " + shape " + std::to_string(sd) + " > " +
                                  std::to_string(traversal_stack_cap) + ")");
     }
@@ -324,7 +325,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
         const shape& s = scn.shapes[si];
         int kinds = (!s.triangles.empty()) + (!s.lines.empty()) + (!s.points.empty());
         if (kinds > 1)
-            throw std::runtime_error("shape " + s.name + " mixes primitive types (unsupported)");
+            throw unsupported_error("shape " + s.name + " mixes primitive types (unsupported)");
         int kind = !s.triangles.empty() ? kind_triangles
                    : !s.lines.empty()   ? kind_lines
                    : !s.points.empty()  ? kind_points
@@ -414,7 +415,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     for (auto& r : wshape_root)
         if (r < 0) r = wempty;
     if (wnodes.size() / 8 * wide_record_bytes >= (1u << 30))
-        throw std::runtime_error("scene too large for the wide any-hit records");
+        throw unsupported_error("scene too large for the wide any-hit records");
     // the wide walk pushes at most three siblings per visit
     ds->wide_ok = 3 * (wtop_depth + wshape_depth) + 2 <= 64;
 
@@ -449,7 +450,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
                     // an inner node's child: the byte offset of its spine record (from the
                     // level's first record), the walks' load offset as is
                     const uint64_t off = (uint64_t)start * spine_record_bytes;
-                    if (off >= (1ull << 31)) throw std::runtime_error("scene too large for the spine records");
+                    if (off >= (1ull << 31)) throw unsupported_error("scene too large for the spine records");
                     lo.w = as_float((int)off);
                 }
                 out.push_back(lo);
@@ -483,7 +484,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
         // .w of the last row: the shape's root node and primitive kind, so a traversal
         // entering the instance needs no dependent fetch of the shape record
         const i4 sh = shapes[ist.shp];
-        if (sh.x >= (1 << 30)) throw std::runtime_error("scene too large (shape nodes >= 2^30, unsupported)");
+        if (sh.x >= (1 << 30)) throw unsupported_error("scene too large (shape nodes >= 2^30, unsupported)");
         tinst.push_back({f.o.x, f.o.y, f.o.z, as_float((int)((uint32_t)sh.x | ((uint32_t)sh.y << 30)))});
     }
 

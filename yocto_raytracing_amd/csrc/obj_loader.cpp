@@ -432,7 +432,7 @@ void load_obj_scene(const std::string& filename, scene& scn) {
         texture t;
         t.path = p;
         if (p.size() >= 4 && p.substr(p.size() - 4) == ".hdr")
-            throw std::runtime_error("hdr textures are not supported: " + p);
+            throw unsupported_error("hdr textures are not supported: " + p);
         bool ok = false;
         auto data = read_file(dir + p, ok);
         std::vector<unsigned char> rgba;

@@ -237,4 +237,14 @@ void save_hdr_or_ldr(const std::string& filename, const float* px, int w, int h)
     fclose(f);
 }
 
+void save_ldr_png(const std::string& filename, const unsigned char* rgba8, int w, int h) {
+    std::vector<unsigned char> png;
+    png_encode_rgba8(rgba8, w, h, png);
+    FILE* f = fopen(filename.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + filename);
+    const size_t wrote = fwrite(png.data(), 1, png.size(), f);
+    fclose(f);
+    if (wrote != png.size()) throw std::runtime_error("cannot write " + filename);
+}
+
 }  // namespace yrt

@@ -11,12 +11,30 @@
 #pragma once
 
 #include <cstdint>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "yrt_math.h"
 
 namespace yrt {
+
+// Typed failures; the C-ABI (capi.cpp guarded()) maps each type to its status code:
+//   unsupported_error -> YRT_ERR_UNSUPPORTED  (input the kernels do not handle)
+//   device_error      -> YRT_ERR_HIP          (a HIP runtime call failed)
+//   device_oom        -> YRT_ERR_OOM          (hipMalloc / hipErrorOutOfMemory)
+//   std::invalid_argument -> YRT_ERR_INVALID_ARG, any other runtime_error -> YRT_ERR_IO
+struct unsupported_error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct device_error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct device_oom : device_error {
+    using device_error::device_error;
+};
+// the message yrt_last_error() reports on this thread (capi.cpp)
+void set_last_error(const std::string& msg);
 
 struct bvh_node {
     bbox3f bbox;     // bounding box
@@ -116,5 +134,7 @@ bool png_encode_rgba8(const unsigned char* rgba, int w, int h, std::vector<unsig
 void tonemap_rgba8(const float* rgba, int w, int h, unsigned char* out);
 // save_hdr_or_ldr (image.cpp:81-88): .hdr -> Radiance RGBE, otherwise PNG of tonemap
 void save_hdr_or_ldr(const std::string& filename, const float* rgba, int w, int h);
+// PNG of an already tonemapped RGBA8 image (the device-tonemap path of yrt_save_image_mem)
+void save_ldr_png(const std::string& filename, const unsigned char* rgba8, int w, int h);
 
 }  // namespace yrt
