@@ -116,6 +116,7 @@ def tonemap_ref(img: np.ndarray) -> np.ndarray:
     x = img[..., :3].astype(np.float32)
     with np.errstate(invalid="ignore"):
         g = np.power(x, np.float32(1 / 2.2)).astype(np.float32)
+    g[np.isneginf(x)] = np.inf  # C pow(-inf, y > 0, y not an odd integer) = +inf; numpy gives NaN
     g = np.where(g > 0, g, np.float32(0))  # max(x, 0): NaN -> 0
     g = np.where(g < 1, g, np.float32(1))
     return (g * np.float32(255)).astype(np.uint8)

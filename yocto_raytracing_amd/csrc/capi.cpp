@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -63,6 +64,17 @@ int guarded(F&& f) {
         g_last_error = "internal error";
         return YRT_ERR_INTERNAL;
     }
+}
+
+// the device tonemap's level thresholds, computed once with this host's powf
+const yrt::tonemap_table& tonemap_table() {
+    static yrt::tonemap_table t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        yrt::tonemap_thresholds(t.thr);
+        t.neg_inf_level = yrt::tonemap_neg_inf_level();
+    });
+    return t;
 }
 
 void* scratch(yrt_scene* s, size_t bytes) {
@@ -355,6 +367,11 @@ int yrt_scene_upload(const yrt_host_scene* hs, int device, yrt_scene** out) {
             s->ds = yrt::device_scene_create(hs->scn, device);
             hip_check(hipMalloc(&s->counters, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long)), "hipMalloc(counters)");
             hip_check(hipMemset(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long)), "hipMemset");
+            // hipMemset of device memory may still be running when it returns, on the null
+            // stream, which a caller's non-blocking stream does not wait for: a first render
+            // on such a stream would race it (seen: a fresh handle's first frame lost part of
+            // k_primary's counts)
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
         } catch (...) {
             yrt_scene_free(s);
             throw;
@@ -540,7 +557,7 @@ int yrt_tonemap(const float* rgba, int n, unsigned char* out, int mem, void* str
     if (n < 0 || (n && (!rgba || !out))) return YRT_ERR_INVALID_ARG;
     return guarded([&] {
         if (mem == YRT_MEM_DEVICE) {
-            hip_check(yrt::launch_tonemap(rgba, n, out, (hipStream_t)stream), "tonemap launch");
+            hip_check(yrt::launch_tonemap(rgba, n, out, tonemap_table(), (hipStream_t)stream), "tonemap launch");
         } else {
             int h = 1;
             yrt::tonemap_rgba8(rgba, n, h, out);
@@ -575,7 +592,7 @@ int yrt_save_image_mem(const char* path, const float* rgba, int w, int h, int me
         unsigned char* d8 = nullptr;
         hip_check(hipMalloc(&d8, n * 4), "hipMalloc(tonemap)");
         std::vector<unsigned char> ldr(n * 4);
-        hipError_t e = yrt::launch_tonemap(rgba, (int)n, d8, st);
+        hipError_t e = yrt::launch_tonemap(rgba, (int)n, d8, tonemap_table(), st);
         if (e == hipSuccess) e = hipMemcpyAsync(ldr.data(), d8, n * 4, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         (void)hipFree(d8);

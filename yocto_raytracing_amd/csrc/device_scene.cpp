@@ -561,6 +561,9 @@ device_scene* device_scene_create(const scene& scn, int device) {
             if (s.bytes)
                 check(hipMemcpy((char*)ds->arena + s.offset, s.src, s.bytes, hipMemcpyHostToDevice),
                       "hipMemcpy(scene)");
+        // the copies ran on the null stream; a caller's non-blocking stream is not ordered
+        // after them, so the upload completes here
+        check(hipDeviceSynchronize(), "hipDeviceSynchronize(scene upload)");
     } catch (...) {
         device_scene_destroy(ds);
         throw;

@@ -232,15 +232,25 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_packet_kernel(dev_scene_vie
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + cnt_rays, s);
 }
 
-// tonemap (image.cpp:55-77): exposure 0, no filmic, gamma 1/2.2, truncating *255
-__global__ void tonemap_kernel(const float4* __restrict__ in, int n, uchar4* __restrict__ out) {
+// tonemap (image.cpp:55-77): exposure 0, no filmic, gamma 1/2.2, truncating *255. A
+// channel's 8-bit value is the number of host thresholds at or below it (tonemap_table:
+// the host powf's exact level boundaries), found by an 8-step bisection; NaN, zero and
+// negative values give 0 as the select clamp does (-inf: pow gives +inf, so 255). Alpha has no pow: computed directly.
+__device__ __forceinline__ unsigned char tonemap_level(const tonemap_table& T, float x) {
+    if (!(x > 0.0f)) return x == -__builtin_inff() ? (unsigned char)T.neg_inf_level : 0;
+    int lo = 0;  // invariant: thr[lo] <= x (thr[0] = 0 < x)
+#pragma unroll
+    for (int step = 128; step >= 1; step >>= 1)
+        if (lo + step < 256 && T.thr[lo + step] <= x) lo += step;
+    return (unsigned char)lo;
+}
+
+__global__ void tonemap_kernel(const float4* __restrict__ in, int n, uchar4* __restrict__ out, tonemap_table T) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     float4 h = in[k];
-    const float g = 1 / 2.2f;
-    float r = powf_cr(h.x, g), gg = powf_cr(h.y, g), b = powf_cr(h.z, g);
-    out[k] = make_uchar4((unsigned char)(sclamp(r, 0.0f, 1.0f) * 255), (unsigned char)(sclamp(gg, 0.0f, 1.0f) * 255),
-                         (unsigned char)(sclamp(b, 0.0f, 1.0f) * 255), (unsigned char)(sclamp(h.w, 0.0f, 1.0f) * 255));
+    out[k] = make_uchar4(tonemap_level(T, h.x), tonemap_level(T, h.y), tonemap_level(T, h.z),
+                         (unsigned char)(sclamp(h.w, 0.0f, 1.0f) * 255));
 }
 
 }  // namespace
@@ -284,10 +294,11 @@ hipError_t launch_trace(const device_scene& ds, const float* rays, int n, int an
     return hipGetLastError();
 }
 
-hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, hipStream_t stream) {
+hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, const tonemap_table& table,
+                          hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, (const float4*)rgba, n,
-                       (uchar4*)out);
+                       (uchar4*)out, table);
     return hipGetLastError();
 }
 

@@ -202,6 +202,37 @@ void tonemap_rgba8(const float* px, int w, int h, unsigned char* out) {
     }
 }
 
+// The 8-bit value of one color channel, (uchar)(clamp(pow(x, 1/2.2), 0, 1) * 255), is a
+// non-decreasing step function of x with this host's powf: it is fully described by
+// the smallest float reaching each level k = 1..255 (found by bisection over the
+// positive float bit patterns, whose integer order is their float order). The device
+// tonemap compares against these and so reproduces the host's libm powf bit for bit,
+// where a device pow could differ by an ulp at a truncation boundary.
+static unsigned char tonemap_channel(float x) {
+    return (unsigned char)(sclamp(std::pow(x, 1 / 2.2f), 0.0f, 1.0f) * 255);
+}
+
+int tonemap_neg_inf_level() { return tonemap_channel(-HUGE_VALF); }
+
+void tonemap_thresholds(float thr[256]) {
+    thr[0] = 0.0f;
+    for (int k = 1; k < 256; k++) {
+        uint32_t lo = 0, hi = 0x7f800000u;  // f(+0) = 0 < k <= 255 = f(+inf)
+        while (hi - lo > 1) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            float x;
+            memcpy(&x, &mid, 4);
+            if (tonemap_channel(x) >= k) hi = mid;
+            else lo = mid;
+        }
+        memcpy(&thr[k], &hi, 4);
+        float below;
+        memcpy(&below, &lo, 4);
+        if (tonemap_channel(thr[k]) < k || tonemap_channel(below) >= k || (k > 1 && thr[k] < thr[k - 1]))
+            throw std::runtime_error("tonemap: host powf is not monotone at level " + std::to_string(k));
+    }
+}
+
 void save_hdr_or_ldr(const std::string& filename, const float* px, int w, int h) {
     FILE* f = fopen(filename.c_str(), "wb");
     if (!f) throw std::runtime_error("cannot write " + filename);

@@ -76,7 +76,14 @@ hipError_t launch_render(device_scene& ds, const dev_render_args& args, void* ou
 hipError_t launch_trace(const device_scene& ds, const float* rays, int n, int any,
                         unsigned char* hit, int* inst, int* ei, float* ew, float* dist,
                         unsigned long long* counters, bool packet, hipStream_t stream);
-hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, hipStream_t stream);
+// tonemap on the device against the host's thresholds (tonemap_thresholds): bit-exact
+// with tonemap_rgba8, i.e. with the host libm's powf
+struct tonemap_table {
+    float thr[256];
+    int neg_inf_level;  // pow(-inf, 1/2.2) = +inf: the one non-positive input that is not 0
+};
+hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, const tonemap_table& table,
+                          hipStream_t stream);
 
 // traversal stack entries per lane (LDS resident): instance level + shape level
 constexpr int traversal_stack_cap = 40;

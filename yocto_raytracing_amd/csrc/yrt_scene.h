@@ -132,6 +132,10 @@ bool png_encode_rgba8(const unsigned char* rgba, int w, int h, std::vector<unsig
 // ---- image helpers (image.cpp) ----
 // tonemap (image.cpp:55-77 with exposure 0, no filmic, srgb): RGBA f32 -> RGBA8
 void tonemap_rgba8(const float* rgba, int w, int h, unsigned char* out);
+// thr[k] (k = 1..255): the smallest float whose tonemapped channel is >= k with this
+// host's powf (thr[0] = 0); the device tonemap's table (scene_io.cpp)
+void tonemap_thresholds(float thr[256]);
+int tonemap_neg_inf_level();  // the level of -inf (pow(-inf, 1/2.2) = +inf)
 // save_hdr_or_ldr (image.cpp:81-88): .hdr -> Radiance RGBE, otherwise PNG of tonemap
 void save_hdr_or_ldr(const std::string& filename, const float* rgba, int w, int h);
 // PNG of an already tonemapped RGBA8 image (the device-tonemap path of yrt_save_image_mem)
