@@ -58,7 +58,7 @@ SALU_PEAK = N_CU * 1.0 * CLOCK_HZ / 1e9   # G wave-instructions/s
 VALU_PEAK = N_CU * 4 * 0.5 * CLOCK_HZ / 1e9
 BAND = 8
 PHASE_KERNEL = {"primary": "k_primary<false, true, unsigned int>",
-                "shadow": "k_shadow<false, true, unsigned int, true>",
+                "shadow": "k_shadow_persist<0>",
                 "shade": "k_shade<false, true, 256, true>",
                 "megakernel": "render_kernel<false>"}
 
@@ -397,7 +397,7 @@ def main():
             bound, pipes, rec = issue
             roof = {"bound": "issue", "pipe": bound, "achieved": pipes[bound]["achieved"],
                     "peak": pipes[bound]["peak"], "unit": "G wave-instructions/s", "frac": pipes[bound]["frac"],
-                    "traffic": traffic, "kernel": PHASE_KERNEL.get(dom, dom), "kernel_ms": kernel_ms,
+                    "traffic": traffic, "kernel": rec.get("kernel", PHASE_KERNEL.get(dom, dom)), "kernel_ms": kernel_ms,
                     "pipes": pipes, "counters": rec.get("source"),
                     "hbm": {"bytes_per_launch": traffic,
                             "achieved_GBs": traffic / (kernel_ms / 1e3) / 1e9 if traffic else None,

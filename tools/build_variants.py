@@ -36,7 +36,7 @@ def main(argv):
             subprocess.run(cmd, check=True, capture_output=True)
             objs.append(o)
         lib = out_dir / f"libyrt_{name}.so"
-        subprocess.run([b.HIPCC, "-shared", "-fPIC", f"--offload-arch={b.ARCH}", "-o", str(lib), *map(str, objs), "-lz"],
+        subprocess.run([b.HIPCC, "-shared", "-fPIC", f"--offload-arch={b.ARCH}", "-o", str(lib), *map(str, objs), *b.LINK_LIBS],
                        check=True)
         print(lib)
 

@@ -24,7 +24,8 @@ import json
 import re
 from pathlib import Path
 
-PHASE_OF = {"k_primary": "primary", "k_shadow": "shadow", "k_shade": "shade", "k_bounce": "bounce",
+PHASE_OF = {"k_primary": "primary", "k_primary_persist": "primary", "k_shadow": "shadow",
+            "k_shadow_persist": "shadow", "k_shade": "shade", "k_bounce": "bounce",
             "k_fold_children": "fold", "k_accumulate": "accumulate", "render_kernel": "megakernel"}
 
 

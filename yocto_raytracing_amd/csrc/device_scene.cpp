@@ -182,8 +182,9 @@ struct wide_builder {
     std::vector<f4>& out;
     int max_depth = 0;
 
-    int emit(const bvh_tree& t, int x, uint32_t leaf_base, int depth) {
-        max_depth = std::max(max_depth, depth);
+    // the slots of the wide node made from binary node x: x's children, each inner child
+    // replaced by its own two children (a leaf root is its own single slot)
+    std::vector<int> slots_of(const bvh_tree& t, int x) const {
         std::vector<int> slots;
         const bvh_node& n = t.nodes[x];
         if (n.isleaf) {
@@ -224,15 +225,24 @@ struct wide_builder {
         else if (YRT_WIDE_SORT != 0)
             std::stable_sort(slots.begin(), slots.end(),
                              [&](int a, int b) { return YRT_WIDE_SORT > 0 ? area(a) > area(b) : area(a) < area(b); });
+        return slots;
+    }
+
+    int alloc() {
         const int me = (int)out.size() / 8;
         out.resize(out.size() + 8, f4{0, 0, 0, 0});
+        return me;
+    }
+
+    // record `me` for `slots`; child(k) gives the record index of inner slot k
+    template <class Child>
+    void write(const bvh_tree& t, int me, const std::vector<int>& slots, uint32_t leaf_base, Child&& child) {
         float v[6][4];
         // child words (yrt_device.h wide_*): an inner child is its record's byte offset,
         // a leaf is leaf bit | count << 28 | first slot; an empty slot is a leaf with no
         // slots behind an inverted infinite box (no finite or infinite ray passes it; a
         // NaN ray, which passes every box, finds nothing there)
         uint32_t word[4] = {wide_leaf, wide_leaf, wide_leaf, wide_leaf};
-        bool inner[4] = {false, false, false, false};
         for (int k = 0; k < 4; k++) {
             if (k >= (int)slots.size()) {
                 for (int a = 0; a < 3; a++) v[a][k] = INFINITY, v[3 + a][k] = -INFINITY;
@@ -247,20 +257,49 @@ struct wide_builder {
                     throw unsupported_error("scene too large for the wide any-hit records");
                 word[k] = wide_leaf | ((uint32_t)s.count << wide_count_shift) | first;
             } else {
-                inner[k] = true;
-            }
-        }
-        for (int k = 0; k < 4; k++)
-            if (inner[k]) {
-                const size_t off = (size_t)emit(t, slots[k], leaf_base, depth + 1) * wide_record_bytes;
+                const size_t off = (size_t)child(k) * wide_record_bytes;
                 if (off > wide_index_mask) throw unsupported_error("scene too large for the wide any-hit records");
                 word[k] = (uint32_t)off;
             }
+        }
         for (int a = 0; a < 6; a++) out[(size_t)me * 8 + a] = {v[a][0], v[a][1], v[a][2], v[a][3]};
         out[(size_t)me * 8 + 6] = {as_float((int)word[0]), as_float((int)word[1]), as_float((int)word[2]),
                                    as_float((int)word[3])};
         out[(size_t)me * 8 + 7] = {as_float((int)slots.size()), 0, 0, 0};
+    }
+
+    // depth first: a node's record, then its inner children's subtrees in slot order
+    int emit(const bvh_tree& t, int x, uint32_t leaf_base, int depth) {
+        max_depth = std::max(max_depth, depth);
+        const std::vector<int> slots = slots_of(t, x);
+        const int me = alloc();
+        int idx[4] = {-1, -1, -1, -1};
+        for (int k = 0; k < (int)slots.size(); k++)
+            if (!t.nodes[slots[k]].isleaf) idx[k] = emit(t, slots[k], leaf_base, depth + 1);
+        write(t, me, slots, leaf_base, [&](int k) { return idx[k]; });
         return me;
+    }
+
+    // breadth first: the records of the top levels come first (the part of the instance
+    // tree the persistent any-hit kernel stages in LDS)
+    int emit_bfs(const bvh_tree& t, int root, uint32_t leaf_base) {
+        struct item {
+            int x, me, depth;
+        };
+        std::vector<item> q = {{root, alloc(), 1}};
+        for (size_t h = 0; h < q.size(); h++) {
+            const item it = q[h];
+            max_depth = std::max(max_depth, it.depth);
+            const std::vector<int> slots = slots_of(t, it.x);
+            int idx[4] = {-1, -1, -1, -1};
+            for (int k = 0; k < (int)slots.size(); k++)
+                if (!t.nodes[slots[k]].isleaf) {
+                    idx[k] = alloc();
+                    q.push_back({slots[k], idx[k], it.depth + 1});
+                }
+            write(t, it.me, slots, leaf_base, [&](int k) { return idx[k]; });
+        }
+        return q.front().me;
     }
 };
 
@@ -393,8 +432,12 @@ device_scene* device_scene_create(const scene& scn, int device) {
     };
     std::vector<f4> wnodes;
     wide_builder wb{wnodes};
-    const int wtop_root = wb.emit(any_tree(scn.bvh), 0, 0, 1);
+#ifndef YRT_WIDE_TOP_BFS
+#define YRT_WIDE_TOP_BFS 1  // instance-level wide records in breadth-first order (top levels first)
+#endif
+    const int wtop_root = YRT_WIDE_TOP_BFS ? wb.emit_bfs(any_tree(scn.bvh), 0, 0) : wb.emit(any_tree(scn.bvh), 0, 0, 1);
     const int wtop_depth = wb.max_depth;
+    const int wtop_records = (int)wnodes.size() / 8;
     std::vector<int> wshape_root(scn.shapes.size());
     int wshape_depth = 0;
     for (size_t si = 0; si < scn.shapes.size(); si++) {
@@ -556,6 +599,11 @@ device_scene* device_scene_create(const scene& scn, int device) {
     try {
         check(hipSetDevice(device), "hipSetDevice");
         check(hipMalloc(&ds->arena, ab.total), "hipMalloc(scene arena)");
+        {
+            int ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+                ds->num_cus = (ncu + 7) / 8 * 8;  // the persistent grids are dealt over 8 XCDs
+        }
         ds->arena_bytes = ab.total;
         for (auto& s : ab.sections)
             if (s.bytes)
@@ -589,6 +637,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);
     v.wtop_root = wtop_root * wide_record_bytes;
+    v.nwtop = wtop_records;
     v.wide = ds->wide_ok ? 1 : 0;
     v.nlights = (int)lights.size() / 6;
     ds->nlights = v.nlights;

@@ -874,107 +874,124 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
 
+// one step of the 4-wide any-hit descent on the record r (in SGPRs when it came through
+// the scalar cache, in VGPRs -- the same value in every lane -- when it came from LDS):
+// the four slab tests, then the first passing child becomes current and the other
+// passing ones are pushed last-to-first (three v_writelane each: word, mask halves), so
+// they pop in slot order. Returns true to continue the descent from `cur`.
+template <int OCT>
+__device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f ci, float tmin, float tmax,
+                                          uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
+                                          int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
+    const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
+                lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
+                hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
+    const uint32_t w[4] = {(uint32_t)uniform(ibits(r[6].x)), (uint32_t)uniform(ibits(r[6].y)),
+                           (uint32_t)uniform(ibits(r[6].z)), (uint32_t)uniform(ibits(r[6].w))};
+    const int nslots = uniform(ibits(r[7].x));
+    unsigned long long m[4];
+    if constexpr (YRT_PK_BOX && OCT < 8) {
+        // slots 0 and 1 always (a leaf root's empty slot 1 fails its test), 2 and 3
+        // when the node has a third slot; a missing fourth is masked out
+        bool p0, p1;
+        box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[0], lx[1]}, f2v{ly[0], ly[1]}, f2v{lz[0], lz[1]},
+                          f2v{hx[0], hx[1]}, f2v{hy[0], hy[1]}, f2v{hz[0], hz[1]}, p0, p1);
+        m[0] = ballot(p0) & mask;
+        m[1] = ballot(p1) & mask;
+        m[2] = m[3] = 0;
+        if (nslots > 2) {
+            bool p2, p3;
+            box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[2], lx[3]}, f2v{ly[2], ly[3]}, f2v{lz[2], lz[3]},
+                              f2v{hx[2], hx[3]}, f2v{hy[2], hy[3]}, f2v{hz[2], hz[3]}, p2, p3);
+            m[2] = ballot(p2) & mask;
+            m[3] = nslots > 3 ? ballot(p3) & mask : 0ull;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!YRT_WIDE_SKIP || k < 2 || k < nslots)  // every wide node has >= 2 slots but a leaf root's 1
+                m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
+            else
+                m[k] = 0;
+        }
+    }
+    unsigned long long cm = 0;
+    uint32_t cw = 0;
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        if (m[k]) {
+            if (cm) {
+                stk_word = writelane(stk_word, (int)cw, sp);
+                stk_mlo = writelane(stk_mlo, (int)(uint32_t)cm, sp);
+                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(cm >> 32), sp);
+                sp++;
+            }
+            cm = m[k];
+            cw = w[k];
+        }
+    }
+    mask = cm;
+    cur = cw;
+#ifdef YRT_EXP_SALU  // sensitivity diagnostic: N extra SALU per wide step (A/B: +8 -> shadow +3.4 %)
+    {
+        int d;
+        asm volatile("s_mov_b32 %0, 0" : "=s"(d));
+#pragma unroll
+        for (int q = 0; q < YRT_EXP_SALU; q++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d) : : "scc");
+        asm volatile("" ::"s"(d));
+    }
+#endif
+#ifdef YRT_EXP_VALU  // sensitivity diagnostic: N extra VALU per wide step (A/B: +8 -> shadow +2.2 %)
+    {
+        float d = co.x;
+#pragma unroll
+        for (int q = 0; q < YRT_EXP_VALU; q++) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
+        asm volatile("" ::"v"(d));
+    }
+#endif
+    if (cm) return !(cw & wide_leaf);
+#if YRT_INNER_POP
+    {
+        int n = 0;
+        if (inner_pop(floor, done, n, mask, sp, stk_word, stk_mlo, stk_mhi)) {
+            cur = (uint32_t)n;
+            return !(cur & wide_leaf);
+        }
+    }
+#endif
+    return false;
+}
+
 // one descent of the 4-wide any-hit walk: from the wide node `cur` (a child word,
 // yrt_device.h) through wide nodes until the current item is a leaf (mask != 0) or no
-// child passes (mask = 0). Children are visited in slot order: the first passing one
-// becomes current, the other passing ones are pushed last-to-first (three v_writelane
-// each: word, mask halves), so they pop in slot order.
-template <int OCT>
-__device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, vec3f ci, float tmin, float tmax,
-                                             uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
-                                             int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
+// child passes (mask = 0). LDSN > 0: the first LDSN records (the breadth-first top of
+// the instance tree, staged by the persistent kernel) are read from `lds` with
+// ds_read_b128 at a wave-uniform address; every other record through the scalar cache.
+template <int OCT, int LDSN>
+__device__ __forceinline__ void wide_descend(const dev_scene_view& S, const float4* lds, vec3f co, vec3f ci,
+                                             float tmin, float tmax, uint32_t& cur, unsigned long long& mask,
+                                             int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
+                                             unsigned long long done) {
     const f4* wbase = sgpr_ptr(S.wnodes);
     for (;;) {
-        float4 r[8];
-        {
+        bool more;
+        if (LDSN > 0 && cur < (uint32_t)(LDSN * wide_record_bytes)) {
+            float4 r[8];
+            const float4* p = lds + (cur >> 4);
+#pragma unroll
+            for (int k = 0; k < 8; k++) r[k] = p[k];
+            more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
+        } else {
+            float4 r[8];
             sgpr16 a, b;
             asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
                          : "=&s"(a), "=&s"(b)
                          : "s"(wbase), "s"(uniform((int)cur)));
 #pragma unroll
             for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
+            more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         }
-        const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
-                    lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
-                    hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
-        const uint32_t w[4] = {(uint32_t)uniform(ibits(r[6].x)), (uint32_t)uniform(ibits(r[6].y)),
-                               (uint32_t)uniform(ibits(r[6].z)), (uint32_t)uniform(ibits(r[6].w))};
-        const int nslots = uniform(ibits(r[7].x));
-        unsigned long long m[4];
-        if constexpr (YRT_PK_BOX && OCT < 8) {
-            // slots 0 and 1 always (a leaf root's empty slot 1 fails its test), 2 and 3
-            // when the node has a third slot; a missing fourth is masked out
-            bool p0, p1;
-            box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[0], lx[1]}, f2v{ly[0], ly[1]}, f2v{lz[0], lz[1]},
-                              f2v{hx[0], hx[1]}, f2v{hy[0], hy[1]}, f2v{hz[0], hz[1]}, p0, p1);
-            m[0] = ballot(p0) & mask;
-            m[1] = ballot(p1) & mask;
-            m[2] = m[3] = 0;
-            if (nslots > 2) {
-                bool p2, p3;
-                box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[2], lx[3]}, f2v{ly[2], ly[3]}, f2v{lz[2], lz[3]},
-                                  f2v{hx[2], hx[3]}, f2v{hy[2], hy[3]}, f2v{hz[2], hz[3]}, p2, p3);
-                m[2] = ballot(p2) & mask;
-                m[3] = nslots > 3 ? ballot(p3) & mask : 0ull;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!YRT_WIDE_SKIP || k < 2 || k < nslots)  // every wide node has >= 2 slots but a leaf root's 1
-                    m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
-                else
-                    m[k] = 0;
-            }
-        }
-        unsigned long long cm = 0;
-        uint32_t cw = 0;
-#pragma unroll
-        for (int k = 3; k >= 0; k--) {
-            if (m[k]) {
-                if (cm) {
-                    stk_word = writelane(stk_word, (int)cw, sp);
-                    stk_mlo = writelane(stk_mlo, (int)(uint32_t)cm, sp);
-                    stk_mhi = writelane(stk_mhi, (int)(uint32_t)(cm >> 32), sp);
-                    sp++;
-                }
-                cm = m[k];
-                cw = w[k];
-            }
-        }
-        mask = cm;
-        cur = cw;
-#ifdef YRT_EXP_SALU  // sensitivity diagnostic: N extra SALU per wide step (A/B: +8 -> shadow +3.4 %)
-        {
-            int d;
-            asm volatile("s_mov_b32 %0, 0" : "=s"(d));
-#pragma unroll
-            for (int q = 0; q < YRT_EXP_SALU; q++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d) : : "scc");
-            asm volatile("" ::"s"(d));
-        }
-#endif
-#ifdef YRT_EXP_VALU  // sensitivity diagnostic: N extra VALU per wide step (A/B: +8 -> shadow +2.2 %)
-        {
-            float d = co.x;
-#pragma unroll
-            for (int q = 0; q < YRT_EXP_VALU; q++) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
-            asm volatile("" ::"v"(d));
-        }
-#endif
-        if (cm) {
-            if (cw & wide_leaf) return;
-            continue;
-        }
-#if YRT_INNER_POP
-        {
-            int n = 0;
-            if (inner_pop(floor, done, n, mask, sp, stk_word, stk_mlo, stk_mhi)) {
-                cur = (uint32_t)n;
-                if (cur & wide_leaf) return;
-                continue;
-            }
-        }
-#endif
-        return;
+        if (!more) return;
     }
 }
 
@@ -986,7 +1003,9 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, vec3f co, 
 // monotone in the box (NaN slabs included), so every leaf reached is one the reference
 // reaches, and the any-hit answer does not depend on the order. The instrumented
 // (COUNT) kernels use the binary walk instead, so work counts stay the reference's.
-__device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid) {
+template <int LDSN = 0>
+__device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid,
+                                                      const float4* lds = nullptr) {
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
@@ -1009,21 +1028,23 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             const int wfloor = level ? base : 0;
             DBG_CHECK(cur < (uint32_t)S.nwnodes * wide_record_bytes && sp >= 0 && sp < 61, 4, (int)cur, sp, level,
                       base, 0);
+#define YRT_WD(o) wide_descend<o, LDSN>(S, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done)
 #if YRT_WIDE_OCTANT
             switch (oct) {
-                case 0: wide_descend<0>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 1: wide_descend<1>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 2: wide_descend<2>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 3: wide_descend<3>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 4: wide_descend<4>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 5: wide_descend<5>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 6: wide_descend<6>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                case 7: wide_descend<7>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
-                default: wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done); break;
+                case 0: YRT_WD(0); break;
+                case 1: YRT_WD(1); break;
+                case 2: YRT_WD(2); break;
+                case 3: YRT_WD(3); break;
+                case 4: YRT_WD(4); break;
+                case 5: YRT_WD(5); break;
+                case 6: YRT_WD(6); break;
+                case 7: YRT_WD(7); break;
+                default: YRT_WD(8); break;
             }
 #else
-            wide_descend<8>(S, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done);
+            YRT_WD(8);
 #endif
+#undef YRT_WD
         }
         // ---- the leaf reached, if any ----
         if (mask) {

@@ -61,6 +61,9 @@ constexpr int shadow_block() { return PACKET ? YRT_SHADOW_BLOCK : WF_BLOCK; }
 #ifndef YRT_PF2
 #define YRT_PF2 1  // closest hit: packet_first (goto-structured walk) instead of packet_trace<false>
 #endif
+#ifndef YRT_SHADOW_GRAB
+#define YRT_SHADOW_GRAB 8  // YRT_SHADOW_PERSIST 2: queue positions taken per atomic (A/B: 2 / 4 / 8 / 32: +82 / -0.8 / -1.9 / +2.4 %)
+#endif
 constexpr int MAX_LEVELS = 16;
 #ifndef YRT_CHUNK_LOG2
 #define YRT_CHUNK_LOG2 29  // samples per chunk, non-reflective scenes (~70 B of HBM each)
@@ -87,6 +90,7 @@ struct wf_buffers {
     f4* rec1[MAX_LEVELS];   // {la.xyz, -}
     f4* rec2[MAX_LEVELS];   // {kr.xyz, -}
     int* count;             // count[k]: rays at level k (k >= 1)
+    unsigned* queue;        // per-XCD work counters of the persistent kernels: [0, 8) shadow, [8, 16) primary
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
 };
@@ -251,20 +255,12 @@ __device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
 }
 
 // ---- level 0: camera rays + closest hit + surface ----
+// the camera samples idx of one wave: eval_camera, closest hit, surface record
 template <bool COUNT, bool PACKET, typename SE>
-__global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A,
-                                                               chunk_args C, wf_buffers B,
-                                                               unsigned long long* counters) {
-    constexpr int BS = YRT_PRIMARY_BLOCK;
-    __shared__ traversal_lds<PACKET, SE> lds;
-    auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
-#if YRT_XCD_CHUNK_PRIMARY && !YRT_XCD_REMAP
-    const int idx = (int)xcd_runs<YRT_XCD_CHUNK_PRIMARY>(blockIdx.x, gridDim.x) * BS + threadIdx.x;
-#else
-    const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
-#endif
+__device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const dev_render_args& A, const chunk_args& C,
+                                                const wf_buffers& B, tracer<false, COUNT, PACKET, SE>& T, int idx,
+                                                work_counts& wc) {
     const int nsamp = C.npix * C.spp;
-    work_counts wc;
     bool valid = false;
     ray3 ray = {{0, 0, 0}, {0, 0, 1}, ray_eps, flt_max};
     if (idx < nsamp) {
@@ -289,8 +285,71 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
         }
         store_surface(B, idx, hit, sf);
     }
+    return valid;
+}
+
+template <bool COUNT, bool PACKET, typename SE>
+__global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A,
+                                                               chunk_args C, wf_buffers B,
+                                                               unsigned long long* counters) {
+    constexpr int BS = YRT_PRIMARY_BLOCK;
+    __shared__ traversal_lds<PACKET, SE> lds;
+    auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
+#if YRT_XCD_CHUNK_PRIMARY && !YRT_XCD_REMAP
+    const int idx = (int)xcd_runs<YRT_XCD_CHUNK_PRIMARY>(blockIdx.x, gridDim.x) * BS + threadIdx.x;
+#else
+    const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
+#endif
+    work_counts wc;
+    const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, idx, wc);
     flush_block<2, BS>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
     if (COUNT) flush_work(counters, wc);
+}
+
+// the same, persistent (YRT_PRIMARY_PERSIST): a resident grid whose waves take the
+// 64-sample blocks from one queue per XCD, YRT_SHADOW_GRAB at a time, in XCD runs of
+// YRT_XCD_CHUNK_PRIMARY blocks (k_shadow_persist's scheme)
+#ifndef YRT_PRIMARY_PERSIST
+#define YRT_PRIMARY_PERSIST 0  // A/B at c4: primary +9 % (runs of 256 or 64 blocks alike)
+#endif
+constexpr int PP_BLOCK = packet_block;  // packet_first parks 1/d per thread in LDS: <= packet_block threads
+template <bool COUNT, bool PACKET, typename SE>
+__global__ __launch_bounds__(PP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(dev_scene_view S, dev_render_args A,
+                                                                              chunk_args C, wf_buffers B, int nblocks,
+                                                                              unsigned long long* counters) {
+    constexpr int WPB = PP_BLOCK / 64;
+    constexpr unsigned RUN = YRT_XCD_CHUNK_PRIMARY > 0 ? YRT_XCD_CHUNK_PRIMARY : 1;
+    constexpr unsigned G = YRT_SHADOW_GRAB;
+    __shared__ traversal_lds<PACKET, SE> lds;
+    auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned xcd = blockIdx.x % 8u;
+    const unsigned n = (unsigned)nblocks;
+    const unsigned full = n / (8u * RUN) * (8u * RUN), per_xcd = full / 8u;
+    auto issue = [&]() -> unsigned {
+        unsigned v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(B.queue + 8 + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+    };
+    unsigned qv = issue(), qb = 0, qleft = 0;
+    unsigned nvalid = 0;  // wave-uniform
+    work_counts wc;
+    for (;;) {
+        if (qleft == 0) {
+            qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
+            qleft = G;
+            qv = issue();
+        }
+        const unsigned q = qb++;
+        qleft--;
+        const unsigned b = q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
+        if (b >= n) break;
+        const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, (int)(b * 64u + lane), wc);
+        nvalid += (unsigned)__popcll(ballot(valid));
+    }
+    (void)WPB;
+    const unsigned long long mine = lane == 0 ? (unsigned long long)nvalid : 0ull;
+    flush_block<2, PP_BLOCK>(counters, {cnt_rays, cnt_samples}, {mine, mine});
 }
 
 // ---- levels >= 1: closest hit of the compacted mirror rays (grid-stride) ----
@@ -393,6 +452,120 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
         flush<true>(counters, cnt_shadow_prim_tests, wc.prim);
         flush<true>(counters, cnt_shadow_wave_node_visits, wc.wnode);
     }
+}
+
+// ---- shadow rays of level 0, persistent: a grid of SP_BLOCK-thread blocks that fills the
+// chip once (YRT_SHADOW_PERSIST); every wave walks its own share of the (64-sample
+// block, light) items, so no block launch, block retirement or per-block counter flush
+// happens per item. LDSN > 0: each block first stages the first LDSN 4-wide records --
+// the breadth-first top of the instance tree (device_scene.cpp emit_bfs) -- in LDS, and
+// the walk reads those with ds_read_b128 instead of through the scalar cache (the
+// north_star's "hot node tiles staged in LDS").
+//
+// Item order: item = bx * nlights + light (the light index minor, as k_shadow). The
+// hardware deals workgroup b to XCD b % 8; XCD x takes runs x, x + 8, x + 16, ... of C
+// consecutive items (k_shadow's XCD runs), its waves interleaved over them, so all eight
+// XCDs sweep the image together while each traces neighbouring pixels. Items past the
+// last whole super-run are dealt round-robin to every wave.
+#ifndef YRT_SHADOW_PERSIST
+#define YRT_SHADOW_PERSIST 2  // 0: one block per item; 1: fixed interleave (A/B +21 %); 2: per-XCD queue (A/B -1.9 %)
+#endif
+#ifndef YRT_SHADOW_LDS_RECORDS
+#define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
+#endif
+#ifndef YRT_SP_BLOCK
+#define YRT_SP_BLOCK 1024  // threads per persistent shadow block (two blocks per CU at 8 waves/SIMD)
+#endif
+constexpr int SP_BLOCK = YRT_SP_BLOCK;
+
+template <int LDSN>
+__global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(dev_scene_view S, int nsamp,
+                                                                                int nx, wf_buffers B,
+                                                                                unsigned long long* counters) {
+    constexpr int WPB = SP_BLOCK / 64;  // waves per block
+    constexpr unsigned C = YRT_SHADOW_LIGHT_MINOR > 0 ? YRT_SHADOW_LIGHT_MINOR : 24;
+    __shared__ float4 lds_nodes[LDSN > 0 ? LDSN * 8 : 1];
+    if constexpr (LDSN > 0) {
+        const int nrec = LDSN * 8;
+        const float4* src = reinterpret_cast<const float4*>(S.wnodes);
+        for (int i = threadIdx.x; i < nrec; i += SP_BLOCK) lds_nodes[i] = src[i];
+        __syncthreads();
+    }
+    const int nl = S.nlights;
+    const unsigned n_items = (unsigned)nx * (unsigned)nl;
+    const unsigned wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned xcd = blockIdx.x % 8u;
+    const unsigned waves_xcd = (gridDim.x / 8u) * WPB;       // gridDim.x is a multiple of 8
+    const unsigned j = (blockIdx.x / 8u) * WPB + wv;          // this wave's index on its XCD
+    const unsigned total_waves = gridDim.x * WPB;
+    const unsigned gw = blockIdx.x * WPB + wv;
+    const unsigned full = n_items / (8u * C) * (8u * C);     // items in whole super-runs
+    const unsigned per_xcd = full / 8u;
+    unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays traced by this wave
+    // YRT_SHADOW_PERSIST 2: the waves of an XCD take the positions of its item sequence
+    // from one agent-scope counter (one atomic per item, issued an item ahead), which
+    // keeps the chip's working window as tight as the hardware's block dealing does;
+    // 1: a fixed interleave (wave j takes j, j + waves_xcd, ...)
+    // the atomic's result stays in lane 0's VGPR until the next item needs it: it is
+    // issued after this item's surface load and before its walk (the walk reads only
+    // through the scalar cache), so its latency hides behind the walk
+    auto issue = [&]() -> unsigned {
+        unsigned v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+    };
+    // YRT_SHADOW_GRAB consecutive positions per atomic (one counter per XCD serialises:
+    // ~11 M atomics/s per address)
+    constexpr unsigned G = YRT_SHADOW_GRAB;
+    unsigned qv = YRT_SHADOW_PERSIST == 2 ? issue() : 0u;  // next batch, lane 0
+    unsigned qb = 0, qleft = 0;                            // current batch (uniform)
+    unsigned qj = j;
+    // q: this wave's position in its XCD's item sequence; every bound is wave-uniform,
+    // so the whole wave reaches every walk
+    for (;;) {
+        unsigned q;
+        if (YRT_SHADOW_PERSIST == 2) {
+            if (qleft == 0) {
+                qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
+                qleft = G;
+                qv = issue();
+            }
+            q = qb++;
+            qleft--;
+        } else {
+            q = qj;
+            qj += waves_xcd;
+        }
+        // runs of C items per XCD, then the tail items past the last whole super-run
+        const unsigned it = q < per_xcd ? ((q / C) * 8u + xcd) * C + q % C : full + (q - per_xcd) * 8u + xcd;
+        if (it >= n_items) break;
+        const int li = (int)(it % (unsigned)nl);
+        const int bx = (int)(it / (unsigned)nl);
+        const f4* lr = S.lights + 6 * li;
+        const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
+        const vec3f lp0 = xyz(ld4(lr + 4));
+        const int idx = bx * 64 + (int)lane;
+        bool valid = false;
+        ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
+        if (idx < nsamp) {
+            float4 s0 = ld4(B.surf0 + idx);
+            if (ibits(s0.w) >= 0) {
+                vec3f p = xyz(s0);
+                vec3f tp = transform_point(lf, lp0 - p);
+                vec3f l = normalize(tp);
+                float r = length(tp);
+                sr = {p, l, 0.01f, r - 0.01f};
+                valid = true;
+            }
+        }
+        rays += (unsigned)__popcll(ballot(valid));
+        const bool occ = packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes);
+        if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
+    }
+    (void)gw;
+    (void)total_waves;
+    const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
+    flush_block<1, SP_BLOCK>(counters, {cnt_shadow_rays}, {mine});
 }
 
 // ---- shade() after the queries (raytrace.cpp:99-206) ----
@@ -632,7 +805,7 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
-    size_t b = align_up(sizeof(int) * (MAX_LEVELS + 1));
+    size_t b = align_up(sizeof(int) * (MAX_LEVELS + 1)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
     if (nlevels > 1) b += (size_t)(nlevels - 1) * 3 * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
     return b;
@@ -648,6 +821,7 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
         return (void*)q;
     };
     B.count = (int*)take(sizeof(int) * (MAX_LEVELS + 1));
+    B.queue = (unsigned*)take(16 * sizeof(unsigned));
     B.surf0 = (f4*)take(16 * c);
     B.surf1 = (f4*)take(16 * c);
     B.surfv = (float*)take(4 * c);
@@ -720,8 +894,17 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         int t = T.begin(phase_primary, stream);
         constexpr int TB = shadow_block<PACKET>();
         const int tgrid = (nsamp + TB - 1) / TB;
-        hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
-                           dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
+        if (YRT_PRIMARY_PERSIST && !COUNT && PACKET) {
+            hipError_t e = hipMemsetAsync(B.queue + 8, 0, 8 * sizeof(unsigned), stream);
+            if (e != hipSuccess) return e;
+            const int nb = ds.num_cus * (YRT_TRACE_WAVES * 4 * 64 / PP_BLOCK);
+            hipLaunchKernelGGL((k_primary_persist<COUNT, PACKET, SE>), dim3(nb), dim3(PP_BLOCK), 0, stream, ds.view,
+                               A, C, B, (nsamp + 63) / 64, counters);
+        } else {
+            hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>),
+                               dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK), dim3(YRT_PRIMARY_BLOCK), 0,
+                               stream, ds.view, A, C, B, counters);
+        }
         T.end(t, stream);
         // levels run: a level with no mirror rays ends the chunk's recursion (the host reads
         // the next level's ray count once per level; the per-level launches it saves cost
@@ -747,7 +930,21 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
-                if (!COUNT && PACKET && ds.wide_ok)
+                if (YRT_SHADOW_PERSIST && !COUNT && PACKET && ds.wide_ok && level == 0 && TB == 64) {
+                    // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
+                    const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
+                    if (YRT_SHADOW_PERSIST == 2) {
+                        hipError_t e = hipMemsetAsync(B.queue, 0, 8 * sizeof(unsigned), stream);
+                        if (e != hipSuccess) return e;
+                    }
+                    constexpr int L = YRT_SHADOW_LDS_RECORDS;
+                    if (L > 0 && ds.view.nwtop >= L)
+                        hipLaunchKernelGGL((k_shadow_persist<L>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
+                                           nsamp, tgrid, B, counters);
+                    else
+                        hipLaunchKernelGGL((k_shadow_persist<0>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
+                                           nsamp, tgrid, B, counters);
+                } else if (!COUNT && PACKET && ds.wide_ok)
                     hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), YRT_EXP_SHADOW_LDS,
                                        stream, ds.view, level, nsamp, B, counters);
                 else

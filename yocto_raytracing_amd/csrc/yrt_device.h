@@ -81,6 +81,7 @@ struct dev_scene_view {
     const f4* spair;  // the same for the shape BVHs (same indexing as snodes)
     const int* tinst_id;
     int wtop_root;
+    int nwtop;  // records of the instance-level wide tree (breadth first: the top levels lead)
     int wide;  // 1: any-hit queries use the 4-wide walk
     int nlights;
     int ntnodes;

@@ -56,6 +56,7 @@ struct device_scene {
     bool reflective = false;   // any material with kr > 0 (bounce levels needed)
     bool wide_ok = false;      // the 4-wide any-hit walk's stack fits (else the binary walk)
     int nlights = 0;
+    int num_cus = 256;  // compute units of the device (persistent grids)
     // wavefront workspace (device), grown on demand
     void* work = nullptr;
     size_t work_bytes = 0;
