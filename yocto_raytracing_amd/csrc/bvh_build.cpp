@@ -12,7 +12,7 @@
 //     centroid box, in-place two-sided (Hoare) partition with the same swap
 //     sequence as std::partition on a bidirectional range (scene.cpp:607-639);
 //     equal_num uses an nth_element median (not used by raytrace, main() passes false)
-// tests/test_bvh.py compares the serialised nodes with the reference's byte-for-byte.
+// tests/test_library.py::test_bvh_matches_reference compares the serialised nodes with the reference's byte-for-byte.
 #include <algorithm>
 #include <stdexcept>
 

@@ -18,7 +18,7 @@
 //       8-bit RGBA textures (stbi_load, req_comp 4), per-instance material = the
 //       shape's material, smooth normals when a shape has none (scene.cpp:11-31)
 // The result is compared byte-for-byte with the reference loader's output
-// (tests/test_loader.py, via the .yrtscene serialisation).
+// (tests/test_library.py::test_obj_loader_matches_reference_loader, via the .yrtscene serialisation).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
