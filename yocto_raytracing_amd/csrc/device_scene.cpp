@@ -503,6 +503,29 @@ device_scene* device_scene_create(const scene& scn, int device) {
                 else
                     y = base + start + 1;
             }
+            if (YRT_FIRST_FILTER) {
+                // the filter boxes: L = X's child start, RL = R's child start (R = X's
+                // child start+1); zero where the parent is a leaf (never read then)
+                static_assert(!YRT_FIRST_FILTER || spine_len == 2, "the filter records extend two-node spines");
+                auto child_start = [&](size_t n) -> long long {
+                    uint32_t c, st;
+                    memcpy(&c, &nodes[2 * n + 1].w, 4);
+                    memcpy(&st, &nodes[2 * n].w, 4);
+                    return (c & leaf_bit) ? -1 : (long long)(base + st);
+                };
+                const long long l = child_start(x);
+                const long long r = l < 0 ? -1 : l + 1;
+                const long long rl = r < 0 ? -1 : child_start((size_t)r);
+                for (long long q : {l, rl}) {
+                    if (q < 0) {
+                        out.push_back({0, 0, 0, 0});
+                        out.push_back({0, 0, 0, 0});
+                    } else {
+                        out.push_back(nodes[2 * q]);
+                        out.push_back(nodes[2 * q + 1]);
+                    }
+                }
+            }
         }
         return out;
     };

@@ -296,7 +296,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
     for (;;) {
         node = uniform(node);  // keep the node index (and the address math) scalar
         float4 rec[2 * spine_len];
-        ld_records_at<2 * spine_len>(pbase, (unsigned)(2 * spine_len * node), rec);
+        ld_records_at<2 * spine_len>(pbase, (unsigned)(spine_record_f4 * node), rec);
         bool pass[spine_len];
 #pragma unroll
         for (int j = 0; j < spine_len; j++) pass[j] = box_hit(co, ci, tmin, tmax, rec[2 * j], rec[2 * j + 1]);
@@ -304,7 +304,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
 #ifdef YRT_EXP_LAT  // diagnostic: one more dependent fetch per step
         {
             float4 again[2];
-            ld_records<2>(pbase + 2 * spine_len * (node ^ (int)(mask & 1)), again);
+            ld_records<2>(pbase + spine_record_f4 * (node ^ (int)(mask & 1)), again);
             asm volatile("" ::"v"(again[0].x));
         }
 #endif
@@ -406,7 +406,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     const uint32_t rk = (uint32_t)uniform(ibits(fo.w));
                     root = (int)(rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
-                    pbase = S.spair + 2 * spine_len * root;
+                    pbase = S.spair + spine_record_f4 * root;
                     cur_slot = k;
                     node = 0;  // the shape root, tested like any popped node
                     mask = inst_mask & ~done;
@@ -633,9 +633,17 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
                                               work_counts& wc, int floor, unsigned long long done) {
+    constexpr bool FILTER = YRT_FIRST_FILTER && !COUNT;  // the instrumented pass counts the reference's tests
     for (;;) {
-        float4 rec[4];
-        {
+        float4 rec[FILTER ? 8 : 4];
+        if constexpr (FILTER) {
+            sgpr16 a, b;
+            asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(a), "=&s"(b)
+                         : "s"(sgpr_ptr(pbase)), "s"(uniform(node)));
+#pragma unroll
+            for (int k = 0; k < 4; k++) rec[k] = rec_of(a, k), rec[4 + k] = rec_of(b, k);
+        } else {
             sgpr16 a;
             asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
                          : "=s"(a)
@@ -666,10 +674,20 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
             node = s0, cl = c0;
             return;
         }
-        stk_node = writelane(stk_node, s0, sp);
-        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
-        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
-        sp++;
+        {
+            // push L (X's child start) for the lanes that passed X; with the filter, only
+            // those that also pass L's box now (its reference test at the pop uses a
+            // tmax no larger than the current one, and the test is monotone in tmax)
+            unsigned long long pl = pm0;
+            if constexpr (FILTER)
+                pl &= ballot(box_oct<OCT>(co, ci, tmin, tmax, rec[4].x, rec[4].y, rec[4].z, rec[5].x, rec[5].y, rec[5].z));
+            if (!FILTER || pl) {
+                stk_node = writelane(stk_node, s0, sp);
+                stk_mlo = writelane(stk_mlo, (int)(uint32_t)pl, sp);
+                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pl >> 32), sp);
+                sp++;
+            }
+        }
         if (COUNT && (pm0 & me)) wc.box++;
         const unsigned long long pm1 = ballot(p1) & pm0;
         mask = pm1;
@@ -685,10 +703,17 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
             node = s1, cl = c1;
             return;
         }
-        stk_node = writelane(stk_node, s1, sp);
-        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
-        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
-        sp++;
+        {
+            unsigned long long prl = pm1;  // RL (R's child start), filtered the same way
+            if constexpr (FILTER)
+                prl &= ballot(box_oct<OCT>(co, ci, tmin, tmax, rec[6].x, rec[6].y, rec[6].z, rec[7].x, rec[7].y, rec[7].z));
+            if (!FILTER || prl) {
+                stk_node = writelane(stk_node, s1, sp);
+                stk_mlo = writelane(stk_mlo, (int)(uint32_t)prl, sp);
+                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(prl >> 32), sp);
+                sp++;
+            }
+        }
         node = s1 + spine_record_bytes;
     }
 }
@@ -824,7 +849,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     co = transform_point_inverse(f, wo);
                     enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[3].w));
-                    pbase = S.spair + 2 * spine_len * (rk & 0x3fffffffu);
+                    pbase = S.spair + spine_record_f4 * (rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
                     cur_slot = k;
                     mask = inst_mask & ~done;

@@ -58,7 +58,14 @@ constexpr int wide_record_bytes = 128;
 constexpr int spine_len = YRT_SPINE;  // nodes per closest-hit walk record (2..4)
 // spine records (tpair/spair): spine_len x {lo, hi} f4 pairs; an inner node's lo.w is
 // the byte offset of its child start's record (child start+1's is the next record)
-constexpr int spine_record_bytes = 32 * spine_len;
+// YRT_FIRST_FILTER: each closest-hit record also carries the boxes of X's child start
+// (L) and of R's child start (RL), so the walk can drop, at push time, the lanes whose
+// later reference test of L / RL must fail (a box test is monotone in tmax); 128 bytes
+#ifndef YRT_FIRST_FILTER
+#define YRT_FIRST_FILTER 0  // A/B at c4: primary +5.4 % (13.43 -> 14.15 ms), identical image
+#endif
+constexpr int spine_record_bytes = YRT_FIRST_FILTER ? 128 : 32 * spine_len;
+constexpr int spine_record_f4 = spine_record_bytes / 16;
 
 struct dev_scene_view {
     const f4* tnodes;
