@@ -895,6 +895,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #define YRT_LEAF_EARLY 0  // any hit: leave a leaf once every lane in it is occluded
 #endif
 
+#ifndef YRT_WIDE_SWITCH
+#define YRT_WIDE_SWITCH 0  // any hit: the passing children pushed by one switch on their 4-bit pattern (A/B: shadow +2.2 %; the switch compiles to a compare tree)
+#endif
 #ifndef YRT_WIDE_SKIP
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
@@ -942,6 +945,36 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
     }
     unsigned long long cm = 0;
     uint32_t cw = 0;
+#if YRT_WIDE_SWITCH
+    // the passing slots as four bits, then one straight-line case per pattern: the lowest
+    // passing slot becomes current, the others are pushed highest first (so they pop in
+    // slot order) at lanes sp, sp+1, ... -- no compare per slot after the bits
+    auto push = [&](int k, int at) {
+        stk_word = writelane(stk_word, (int)w[k], sp + at);
+        stk_mlo = writelane(stk_mlo, (int)(uint32_t)m[k], sp + at);
+        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m[k] >> 32), sp + at);
+    };
+    const unsigned bits = (m[0] ? 1u : 0u) | (m[1] ? 2u : 0u) | (m[2] ? 4u : 0u) | (m[3] ? 8u : 0u);
+    switch (bits) {
+        case 0: cm = 0; cw = 0; break;
+        case 1: cm = m[0]; cw = w[0]; break;
+        case 2: cm = m[1]; cw = w[1]; break;
+        case 3: push(1, 0); sp += 1; cm = m[0]; cw = w[0]; break;
+        case 4: cm = m[2]; cw = w[2]; break;
+        case 5: push(2, 0); sp += 1; cm = m[0]; cw = w[0]; break;
+        case 6: push(2, 0); sp += 1; cm = m[1]; cw = w[1]; break;
+        case 7: push(2, 0); push(1, 1); sp += 2; cm = m[0]; cw = w[0]; break;
+        case 8: cm = m[3]; cw = w[3]; break;
+        case 9: push(3, 0); sp += 1; cm = m[0]; cw = w[0]; break;
+        case 10: push(3, 0); sp += 1; cm = m[1]; cw = w[1]; break;
+        case 11: push(3, 0); push(1, 1); sp += 2; cm = m[0]; cw = w[0]; break;
+        case 12: push(3, 0); sp += 1; cm = m[2]; cw = w[2]; break;
+        case 13: push(3, 0); push(2, 1); sp += 2; cm = m[0]; cw = w[0]; break;
+        case 14: push(3, 0); push(2, 1); sp += 2; cm = m[1]; cw = w[1]; break;
+        case 15: push(3, 0); push(2, 1); push(1, 2); sp += 3; cm = m[0]; cw = w[0]; break;
+        default: break;
+    }
+#else
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
         if (m[k]) {
@@ -955,6 +988,7 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
             cw = w[k];
         }
     }
+#endif
     mask = cm;
     cur = cw;
 #ifdef YRT_EXP_SALU  // sensitivity diagnostic: N extra SALU per wide step (A/B: +8 -> shadow +3.4 %)

@@ -281,7 +281,12 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     if (valid) {
         surface sf = {};
         if (hit) {
+#ifdef YRT_EXP_NOSURF  // timing diagnostic only (the image is wrong): the walk without the surface
+            sf.p = {hr.dist, hr.ew.y, hr.ew.z};
+            sf.mat = hr.slot & 3;
+#else
             sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
+#endif
             if (COUNT) wc.hits++;
         }
         store_surface(B, idx, hit, sf);
