@@ -50,11 +50,11 @@ def test_binding_hands_over_the_reference_scene(name, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not INT_SO.exists(), reason="oracle/_ref/libyrtref_int.so not built (make -C oracle ref)")
-@pytest.mark.parametrize("name", ["basic", "refl", "lines"])
+@pytest.mark.parametrize("name", ["basic", "simple", "refl", "instance10000", "lines"])
 def test_raytrace_gpu_from_reference_scene(name):
     lib = int_lib()
     z = np.load(GOLDEN / f"ref_render_{name}.npz")
-    key = sorted(k for k in z.files if k.startswith("img_"))[0]
+    key = max((k for k in z.files if k.startswith("img_")), key=lambda k: z[k].size)  # the largest fixture
     _, r, s = key.split("_")
     res, spp = int(r[1:]), int(s[1:])
     ref = z[key]
