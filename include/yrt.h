@@ -118,6 +118,10 @@ int yrt_scene_load(const char* path, yrt_host_scene** out);
 int yrt_scene_save(const yrt_host_scene* hs, const char* path);
 /* build_bvh(scene*, bool equal_num) (src/scene.cpp:554-565, decl scene.h:238) */
 int yrt_host_scene_build_bvh(yrt_host_scene* hs, int equal_num);
+/* build_bvh with the tree construction (node boxes, splits, partitions) on GPU `device`:
+ * the same nodes and leaf order as yrt_host_scene_build_bvh, byte for byte. equal_num != 0
+ * is YRT_ERR_UNSUPPORTED. kernel_ms (may be NULL): GPU time of the build's level passes */
+int yrt_host_scene_build_bvh_gpu(yrt_host_scene* hs, int equal_num, int device, float* kernel_ms);
 /* dump the BVHs (.yrtbvh) byte-compatible with the reference's bvh_node (scene.h:9-15) */
 int yrt_host_scene_save_bvh(const yrt_host_scene* hs, const char* path);
 /* counts: [cameras, textures, materials, shapes, instances, lights, bvh nodes(instance

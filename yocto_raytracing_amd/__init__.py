@@ -265,9 +265,17 @@ def load_scene(filename: str) -> Scene:
     return Scene(h.value)
 
 
-def build_bvh(scn: Scene, equal_num: bool = False) -> None:
-    """build_bvh (src/scene.cpp:554): per-shape BVHs, then the instance BVH."""
-    check(N.lib.yrt_host_scene_build_bvh(scn.handle, 1 if equal_num else 0), "build_bvh")
+def build_bvh(scn: Scene, equal_num: bool = False, device: Optional[int] = None) -> Optional[float]:
+    """build_bvh (src/scene.cpp:554): per-shape BVHs, then the instance BVH. With
+    `device`, the tree construction runs on that GPU (the same nodes byte for byte) and
+    the GPU milliseconds of its level passes are returned."""
+    if device is None:
+        check(N.lib.yrt_host_scene_build_bvh(scn.handle, 1 if equal_num else 0), "build_bvh")
+        return None
+    ms = C.c_float(0)
+    check(N.lib.yrt_host_scene_build_bvh_gpu(scn.handle, 1 if equal_num else 0, int(device), C.byref(ms)),
+          "build_bvh(device)")
+    return float(ms.value)
 
 
 def render_params(amb=(0.1, 0.1, 0.1), resolution: int = 720, samples: int = 1, *,

@@ -84,6 +84,7 @@ _sig = {
     "yrt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "yrt_scene_save": (C.c_int, [_vp, C.c_char_p]),
     "yrt_host_scene_build_bvh": (C.c_int, [_vp, C.c_int]),
+    "yrt_host_scene_build_bvh_gpu": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "yrt_host_scene_save_bvh": (C.c_int, [_vp, C.c_char_p]),
     "yrt_host_scene_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
     "yrt_host_image_size": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),

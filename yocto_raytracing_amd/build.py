@@ -27,7 +27,7 @@ CLANGXX = os.environ.get("YRT_CXX", "/opt/rocm/lib/llvm/bin/clang++")
 ARCH = os.environ.get("YRT_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["obj_loader.cpp", "png.cpp", "scene_io.cpp", "bvh_build.cpp",
-           "device_scene.cpp", "capi.cpp", "multi.cpp", "render.hip", "wavefront.hip"]
+           "device_scene.cpp", "capi.cpp", "multi.cpp", "render.hip", "wavefront.hip", "bvh_gpu.hip"]
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           f"-I{CSRC}", f"-I{ROOT / 'include'}"]
 

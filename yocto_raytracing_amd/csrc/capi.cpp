@@ -194,6 +194,20 @@ int yrt_host_scene_build_bvh(yrt_host_scene* hs, int equal_num) {
     });
 }
 
+int yrt_host_scene_build_bvh_gpu(yrt_host_scene* hs, int equal_num, int device, float* kernel_ms) {
+    if (!hs) return YRT_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        g_last_error = "no HIP device visible";
+        return YRT_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= ndev) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::build_bvh_gpu(hs->scn, equal_num != 0, device, kernel_ms);
+        return YRT_OK;
+    });
+}
+
 int yrt_host_scene_save_bvh(const yrt_host_scene* hs, const char* path) {
     if (!hs || !path) return YRT_ERR_INVALID_ARG;
     if (!hs->scn.has_bvh) {

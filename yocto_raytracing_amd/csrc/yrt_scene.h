@@ -121,6 +121,9 @@ void save_yrtbvh(const std::string& filename, const scene& scn);
 
 // ---- BVH (bvh_build.cpp): restates build_bvh (src/scene.cpp:509-658) ----
 void build_bvh(scene& scn, bool equal_num);
+// the same nodes, byte for byte, with the tree construction on GPU `device`
+// (bvh_gpu.hip); kernel_ms (optional): device time of the level passes
+void build_bvh_gpu(scene& scn, bool equal_num, int device, float* kernel_ms);
 int bvh_max_depth(const bvh_tree& bvh);
 
 // ---- PNG (png.cpp) ----
