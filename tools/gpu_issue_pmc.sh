@@ -20,7 +20,7 @@ groups=(
 i=0
 for g in "${groups[@]}"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $g --output-format csv -d $OUT/p$i -o p$i -- python3 $B > $OUT/p$i.log 2>&1
+  timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $g --output-format csv -d $OUT/p$i -o p$i -- python3 $B > $OUT/p$i.log 2>&1
   rc=$?
   echo "pass $i ($g): rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi

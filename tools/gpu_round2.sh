@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-2 evidence on one GPU box, in two calls (each under gpurun's 20-minute limit):
+#   bash tools/gpu_round2.sh A TAG   -m gpu suite, smoke, c4 counters + kernel stats, the
+#                                    default bench line (CPU baselines), N=2 rehearsal
+#   bash tools/gpu_round2.sh B TAG   c3 and c5 counters + bench lines
+# Every GPU step has its own time limit; a failing step ends the script. The counter
+# summaries are written to gpurun_out/TAG/ (and into this copy's profiles/, so the bench
+# lines that follow carry the issue roofline).
+set -u
+PART=$1; TAG=$2
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+run() { "$@"; local rc=$?; if [ $rc -ne 0 ]; then echo "FAILED (rc=$rc): $*"; exit $rc; fi; }
+summ() {  # key, pmc dir
+  run python tools/pmc_summary.py --key $1 --csv $2/p*/p*_counter_collection.csv --source profiles/r2/$TAG \
+      --traffic profiles/pmc_traffic.json --issue profiles/issue_counters.json > $2/summary.json
+  cp profiles/pmc_traffic.json profiles/issue_counters.json $OUT/
+}
+if [ "$PART" = A ]; then
+  run timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+  tail -n 2 $OUT/pytest.log
+  run timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+  run bash tools/gpu_issue_pmc.sh $TAG/pmc_c4 > $OUT/pmc_c4.log 2>&1
+  summ instance10000-1920x1080-s8-n1-wavefront $OUT/pmc_c4
+  run timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+  cat $OUT/bench.json
+  YRT_BENCH_DEVICES=1 YRT_BENCH_BACKEND=gloo YRT_BENCH_OVERLAP=1 run timeout -k 10 400 \
+    python bench.py --gpus 2 --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/bench_n2_rehearsal_gloo_1gpu.json 2> $OUT/n2.err
+  grep -h '^{' $OUT/bench_n2_rehearsal_gloo_1gpu.json | cut -c1-300
+else
+  PMC_TIMEOUT=200 run bash tools/gpu_issue_pmc.sh $TAG/pmc_c3 --scene refl --resolution 1080 --samples 4 > $OUT/pmc_c3.log 2>&1
+  summ refl-1920x1080-s4-n1-wavefront $OUT/pmc_c3
+  PMC_TIMEOUT=300 run bash tools/gpu_issue_pmc.sh $TAG/pmc_c5 --resolution 4096 --width 4096 --samples 16 > $OUT/pmc_c5.log 2>&1
+  summ instance10000-4096x4096-s16-n1-wavefront $OUT/pmc_c5
+  run timeout -k 10 300 python bench.py --scene refl --resolution 1080 --samples 4 --cpu-seconds 0 > $OUT/bench_c3_refl.json 2> $OUT/c3.err
+  run timeout -k 10 400 python bench.py --resolution 4096 --width 4096 --samples 16 --steps 2 --warmup 1 --cpu-seconds 6 > $OUT/bench_c5_1gpu.json 2> $OUT/c5.err
+  cut -c1-400 $OUT/bench_c3_refl.json $OUT/bench_c5_1gpu.json
+fi

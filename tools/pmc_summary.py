@@ -36,19 +36,28 @@ def short(name: str) -> str:
 
 
 def per_launch(paths) -> dict:
-    """{kernel: {counter: mean value per dispatch}}"""
+    """{phase: {counter: mean value per dispatch}, "_kernels": {phase: [kernel names]}} over
+    the timed kernels of each phase (a reflective frame's shadow phase has one persistent
+    level-0 launch and one grid-stride launch per mirror level: their mean per launch is
+    what bench.py's per-launch time is set against)"""
     vals = collections.defaultdict(float)
     launches = collections.defaultdict(set)
+    kernels = collections.defaultdict(set)
     for path in paths:
         for r in csv.DictReader(open(path)):
             k = short(r["Kernel_Name"])
             if re.match(r"\w+<true", k):  # COUNT=true: the instrumented twin
                 continue
-            vals[(k, r["Counter_Name"])] += float(r["Counter_Value"])
-            launches[(k, r["Counter_Name"])].add((path, r["Dispatch_Id"]))
+            phase = PHASE_OF.get(k.split("<")[0])
+            if not phase:
+                continue
+            kernels[phase].add(k)
+            vals[(phase, r["Counter_Name"])] += float(r["Counter_Value"])
+            launches[(phase, r["Counter_Name"])].add((path, r["Dispatch_Id"]))
     out = collections.defaultdict(dict)
-    for (k, c), v in vals.items():
-        out[k][c] = v / max(1, len(launches[(k, c)]))
+    for (ph, c), v in vals.items():
+        out[ph][c] = v / max(1, len(launches[(ph, c)]))
+    out["_kernels"] = {ph: sorted(ks) for ph, ks in kernels.items()}
     return out
 
 
@@ -63,10 +72,9 @@ def main():
     data = per_launch(a.csv)
     traffic = json.loads(Path(a.traffic).read_text()) if Path(a.traffic).exists() else {}
     issue = json.loads(Path(a.issue).read_text()) if Path(a.issue).exists() else {}
-    for k, c in sorted(data.items()):
-        phase = PHASE_OF.get(k.split("<")[0])
-        if not phase:
-            continue
+    names = data.pop("_kernels")
+    for phase, c in sorted(data.items()):
+        k = " + ".join(names.get(phase, [])) or phase
         key = f"{a.key}-{phase}"
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             f, w = c["FETCH_SIZE"], c["WRITE_SIZE"]
