@@ -657,6 +657,12 @@ __global__ __launch_bounds__(SD_BLOCK, YRT_SHADOW_DUAL_WAVES) void k_shadow_dual
 #ifndef YRT_SHADE_SMAT
 #define YRT_SHADE_SMAT 0  // k_shade: a wave-uniform material record through the scalar cache (A/B: c4 shade +12 %)
 #endif
+#ifndef YRT_EAGER_FOLD
+#define YRT_EAGER_FOLD 1  // reflective scenes: k_shade folds final values up the mirror chain (no k_fold_children)
+#endif
+#ifndef YRT_SHADE_SLIGHT
+#define YRT_SHADE_SLIGHT 1  // k_shade: light records through the scalar cache
+#endif
 #ifndef YRT_SHADE_OCC4
 #define YRT_SHADE_OCC4 1  // k_shade: occlusion bytes of <= 4 lights loaded with the surface
 #endif
@@ -736,8 +742,17 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 for (int li = 0; li < S.nlights; li++) {
                     if (OCC4 ? ((occ_bits >> li) & 1u) != 0u : B.occl[(size_t)li * B.capacity + idx] != 0) continue;
                     const f4* lr = S.lights + 6 * li;
+#if YRT_SHADE_SLIGHT
+                    // the light record is the same for every lane (li is the loop index):
+                    // one scalar fetch instead of six 64-lane vector loads of one address
+                    float4 lrec[6];
+                    ld_scalar<6>(lr, lrec);
+                    frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
+                    vec3f lp0 = xyz(lrec[4]), ke = xyz(lrec[5]);
+#else
                     frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
                     vec3f lp0 = xyz(ld4(lr + 4)), ke = xyz(ld4(lr + 5));
+#endif
                     vec3f tp = transform_point(lf, lp0 - p);
                     vec3f l = normalize(tp);
                     float r = length(tp);
@@ -782,8 +797,27 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
             if (FUSE) {
                 fused_rad[threadIdx.x] = make_float4(R.x, R.y, R.z, 1.0f);
             } else if (write_r) {
+#if YRT_EAGER_FOLD
+                // a final value at level k >= 1 folds straight up its chain of parents
+                // (raytrace.cpp:201-206, R_k-1 = (D + R_k * kr) + la, in that order) to
+                // the camera sample; each parent has this one child, so its value is
+                // final now too
+                vec3f col = R;
+                int lev = level, node = idx;
+                while (lev > 0) {
+                    const int parent = ibits(B.ray_o[lev][node].w);
+                    const float4 d = ld4(B.rec0[lev - 1] + parent), la = ld4(B.rec1[lev - 1] + parent),
+                                 kr = ld4(B.rec2[lev - 1] + parent);
+                    vec3f cc = {d.x, d.y, d.z};
+                    cc = cc + vec3f{col.x * kr.x, col.y * kr.y, col.z * kr.z};
+                    cc = cc + xyz(la);
+                    col = cc, node = parent, lev--;
+                }
+                B.rad[node] = {col.x, col.y, col.z, 1.0f};
+#else
                 f4* dst = level ? B.R[level] : B.rad;
                 dst[idx] = {R.x, R.y, R.z, 1.0f};
+#endif
             }
         }
         // compaction of the mirror rays: one atomic per BLOCK (a shared counter hit by
@@ -858,26 +892,42 @@ __global__ __launch_bounds__(WF_BLOCK) void k_fold_children(int level, wf_buffer
 }
 
 // ---- ordered per-pixel sum (raytrace.cpp:232-249) ----
+// A wave sums 64 pixels. Their samples are consecutive in memory (spp per pixel), so the
+// wave stages them through LDS AQ samples of every pixel at a time with loads in which
+// neighbouring lanes read neighbouring samples (a pixel's AQ samples are one contiguous
+// run), then each lane adds its own pixel's samples in the reference's order.
+constexpr int AQ = 8;
 __global__ __launch_bounds__(WF_BLOCK) void k_accumulate(dev_render_args A, chunk_args C, wf_buffers B,
                                                          float4* __restrict__ out) {
-    const int pl = blockIdx.x * WF_BLOCK + threadIdx.x;
-    if (pl >= C.npix) return;
-    int lx, ly, i, j;
-    const long long p = C.pix0 + pl;
-    bool valid = pixel_of(A, C.tiles_x, p, lx, ly, i, j);
-    if (lx >= A.tile_w || ly >= A.tile_h) return;
-    if (!valid) {
-        out[(size_t)ly * A.out_stride + lx] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        return;
-    }
+    __shared__ float4 stage[WF_BLOCK / 64][64 * (AQ + 1)];  // rows padded against bank conflicts
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pl0 = blockIdx.x * WF_BLOCK + w * 64;
+    const int np = max(0, min(64, C.npix - pl0));  // pixels of this wave
+    float4* S = stage[w];
+    const f4* base = B.rad + (size_t)pl0 * C.spp;
     vec4f acc = {0, 0, 0, 0};
-    const f4* r = B.rad + (size_t)pl * C.spp;
-    for (int q = 0; q < C.spp; q++) {
-        float4 c = ld4(r + q);
-        acc = {acc.x + c.x, acc.y + c.y, acc.z + c.z, acc.w + 1.0f};
+    for (int q0 = 0; q0 < C.spp; q0 += AQ) {  // the same trip count in every wave of the block
+        const int qn = min(AQ, C.spp - q0);
+        for (int e = lane; e < np * qn; e += 64) {
+            const int px = e / qn, q = e % qn;
+            S[px * (AQ + 1) + q] = ld4(base + (size_t)px * C.spp + q0 + q);
+        }
+        __syncthreads();
+        if (lane < np)
+            for (int q = 0; q < qn; q++) {
+                const float4 c = S[lane * (AQ + 1) + q];
+                acc = {acc.x + c.x, acc.y + c.y, acc.z + c.z, acc.w + 1.0f};
+            }
+        __syncthreads();
     }
+    if (lane >= np) return;
+    const int pl = pl0 + lane;
+    int lx, ly, i, j;
+    const bool valid = pixel_of(A, C.tiles_x, C.pix0 + pl, lx, ly, i, j);
+    if (lx >= A.tile_w || ly >= A.tile_h) return;
     const float d = float(C.spp);
-    out[(size_t)ly * A.out_stride + lx] = make_float4(acc.x / d, acc.y / d, acc.z / d, 1.0f);
+    out[(size_t)ly * A.out_stride + lx] =
+        valid ? make_float4(acc.x / d, acc.y / d, acc.z / d, 1.0f) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -886,7 +936,9 @@ size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
     size_t b = align_up(sizeof(int) * (MAX_LEVELS + 1)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
-    if (nlevels > 1) b += (size_t)(nlevels - 1) * 3 * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
+    // levels >= 1: ray_o, ray_d (+ R without the eager fold); levels < last: rec0..2
+    if (nlevels > 1)
+        b += (size_t)(nlevels - 1) * (YRT_EAGER_FOLD ? 2 : 3) * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
     return b;
 }
 
@@ -909,7 +961,7 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
     for (int k = 1; k < nlevels; k++) {
         B.ray_o[k] = (f4*)take(16 * c);
         B.ray_d[k] = (f4*)take(16 * c);
-        B.R[k] = (f4*)take(16 * c);
+        B.R[k] = YRT_EAGER_FOLD ? nullptr : (f4*)take(16 * c);
     }
     for (int k = 0; k + 1 < nlevels; k++) {
         B.rec0[k] = (f4*)take(16 * c);
@@ -1059,7 +1111,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
 #undef YRT_SHADE_LAUNCH
             T.end(t, stream);
         }
-        for (int level = levels_run - 2; level >= 0; level--) {
+        for (int level = YRT_EAGER_FOLD ? -1 : levels_run - 2; level >= 0; level--) {
             t = T.begin(phase_fold, stream);
             hipLaunchKernelGGL(k_fold_children, dim3(stride_grid), dim3(WF_BLOCK), 0, stream, level, B);
             T.end(t, stream);
