@@ -476,6 +476,9 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #ifndef YRT_SHADOW_PERSIST
 #define YRT_SHADOW_PERSIST 2  // 0: one block per item; 1: fixed interleave (A/B +21 %); 2: per-XCD queue (A/B -1.9 %)
 #endif
+#ifndef YRT_SHADOW_PERSIST_LEVELS
+#define YRT_SHADOW_PERSIST_LEVELS 0  // the persistent shadow kernel for the mirror levels too (A/B at c3: shadow +32 %)
+#endif
 #ifndef YRT_SHADOW_LDS_RECORDS
 #define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
 #endif
@@ -498,6 +501,12 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         __syncthreads();
     }
     const int nl = S.nlights;
+    // level >= 1 (level passed as -level - 1 in nsamp): the compacted mirror-hit samples,
+    // counted on the device by the level's k_bounce
+    if (nsamp < 0) {
+        nsamp = B.count[-nsamp - 1];
+        nx = (nsamp + 63) / 64;
+    }
     const unsigned n_items = (unsigned)nx * (unsigned)nl;
     const unsigned wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
@@ -1067,7 +1076,8 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                     const int nb = ds.num_cus * (YRT_SHADOW_DUAL_WAVES * 4 * 64 / SD_BLOCK);
                     hipLaunchKernelGGL(k_shadow_dual, dim3(nb), dim3(SD_BLOCK), 0, stream, ds.view, nsamp, tgrid, B,
                                        counters);
-                } else if (YRT_SHADOW_PERSIST && !COUNT && PACKET && ds.wide_ok && level == 0 && TB == 64) {
+                } else if (YRT_SHADOW_PERSIST && !COUNT && PACKET && ds.wide_ok && TB == 64 &&
+                           (level == 0 || YRT_SHADOW_PERSIST_LEVELS)) {
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
                     if (YRT_SHADOW_PERSIST == 2) {
@@ -1077,10 +1087,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                     constexpr int L = YRT_SHADOW_LDS_RECORDS;
                     if (L > 0 && ds.view.nwtop >= L)
                         hipLaunchKernelGGL((k_shadow_persist<L>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
-                                           nsamp, tgrid, B, counters);
+                                           level ? -level - 1 : nsamp, tgrid, B, counters);
                     else
                         hipLaunchKernelGGL((k_shadow_persist<0>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
-                                           nsamp, tgrid, B, counters);
+                                           level ? -level - 1 : nsamp, tgrid, B, counters);
                 } else if (!COUNT && PACKET && ds.wide_ok)
                     hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), YRT_EXP_SHADOW_LDS,
                                        stream, ds.view, level, nsamp, B, counters);
