@@ -224,13 +224,21 @@ def cpu_baseline_all_cores(scene_file: Path, res: int, width: int, spp_axis: int
 
 # ---------------------------------------------------------------- roofline
 
-def issue_roofline(issue_json: Path, key: str, kernel_ms: float):
+def issue_roofline(issue_json: Path, key: str, kernel_ms: float, key_n1: str = "", share: float = 1.0):
     """achieved issue rate of the dominant kernel: its committed per-launch instruction
-    counts / the live launch time"""
+    counts / the live launch time. At N > 1 ranks without counters of that exact run, the
+    single-GPU counts of the same frame are scaled by this rank's share of the frame's rays
+    (the walks' instruction counts follow the rays they trace; the result says so)."""
     try:
-        rec = json.loads(issue_json.read_text()).get(key)
+        table = json.loads(issue_json.read_text())
     except (OSError, ValueError):
-        rec = None
+        table = {}
+    rec = table.get(key)
+    if rec is None and key_n1 and key_n1 in table:
+        rec = dict(table[key_n1])
+        for c in ("SQ_INSTS_SALU", "SQ_INSTS_VALU"):
+            rec[c] = rec[c] * share
+        rec["source"] = f"{rec.get('source')} (n1 counts x this rank's ray share {share:.4f})"
     if not rec or kernel_ms <= 0:
         return None
     s = kernel_ms / 1e3
@@ -392,7 +400,9 @@ def main():
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-        issue = issue_roofline(Path(a.issue_json), key, kernel_ms)
+        key_n1 = f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-{dom}"
+        share = (st["rays"] * a.steps) / total_rays if total_rays else 1.0  # rank 0's share of the frame
+        issue = issue_roofline(Path(a.issue_json), key, kernel_ms, key_n1, share)
         if issue:
             bound, pipes, rec = issue
             roof = {"bound": "issue", "pipe": bound, "achieved": pipes[bound]["achieved"],
