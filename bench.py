@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     p.add_argument("--issue-json", default=str(ROOT / "profiles" / "issue_counters.json"))
     p.add_argument("--algorithm", default="wavefront", choices=("wavefront", "megakernel", "wavefront_lane"))
+    p.add_argument("--profile-rank", default="",
+                   help="R/N: one process renders rank R's bands of an N-rank run, no gather (the counter "
+                        "passes for the N-rank roofline, tools/gpu_issue_pmc.sh); its line is not a bench result")
     p.add_argument("--dry-run", action="store_true",
                    help="launch/rendezvous/report only, no GPU work (tests the N-rank launcher on CPU)")
     return p.parse_args()
@@ -301,8 +304,15 @@ def main():
 
     params = yrt.render_params(0.1, a.resolution, a.samples, width=a.width, algorithm=a.algorithm)
     W, H = ds.image_size(params)
-    layout = BandLayout(H, world, BAND)
-    band, local_rows = render_params_band(layout, rank)
+    band_world, band_rank = world, rank
+    if a.profile_rank:
+        if world > 1:
+            raise SystemExit("--profile-rank is a single-process mode")
+        band_rank, band_world = (int(v) for v in a.profile_rank.split("/"))
+        if not 0 <= band_rank < band_world:
+            raise SystemExit(f"--profile-rank {a.profile_rank}: want R/N with 0 <= R < N")
+    layout = BandLayout(H, band_world, BAND)
+    band, local_rows = render_params_band(layout, band_rank)
     params.band, params.band_stride, params.band_offset = band
     params.tile_h = local_rows  # every rank renders the same padded count (rows past H read 0)
     # two frames in flight at N > 1 over RCCL: frame i's all_gather + reassembly run on a
@@ -325,7 +335,8 @@ def main():
         params.timing = timing
         if not overlap:
             ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
-            gather_frame(shards[b], layout, index, gathered[b], frames[b])
+            if not a.profile_rank:
+                gather_frame(shards[b], layout, index, gathered[b], frames[b])
             return b
         if gathered_ev[b] is not None:  # shards[b] is free once its previous gather has read it
             stream.wait_event(gathered_ev[b])
@@ -392,7 +403,7 @@ def main():
         spp = a.samples * a.samples
         is_c4 = (a.scene, a.resolution, a.width, a.samples) == ("instance10000", 1080, 0, 8)
         metric = BASELINE_METRIC if is_c4 else f"Mrays/sec + ms/frame, {a.scene} {W}×{H}×{spp}spp, {world} MI355X"
-        key = f"{a.scene}-{W}x{H}-s{a.samples}-n{world}-{a.algorithm}-{dom}"
+        key = f"{a.scene}-{W}x{H}-s{a.samples}-n{band_world}-{a.algorithm}-{dom}"
         kernel_ms = dom_ms / dom_launches
         traffic = None
         try:
@@ -448,7 +459,10 @@ def main():
                        "algorithm": a.algorithm},
             "roofline": roof,
         }
-        if world == 1 and a.cpu_seconds > 0:
+        if a.profile_rank:  # a counter-collection run, not a bench result
+            line["metric"] = f"profile of rank {a.profile_rank} (bands only, no gather): {metric}"
+            line["config"]["parallelism"] = f"rank {a.profile_rank} of an image-band split, rendered alone"
+        if world == 1 and a.cpu_seconds > 0 and not a.profile_rank:
             line["cpu_baseline"] = cpu_baseline(scene_file, a.resolution, a.width, a.samples, a.cpu_seconds)
             line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(scene_file, a.resolution, a.width, a.samples,
                                                                     a.cpu_seconds)

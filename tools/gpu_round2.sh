@@ -3,6 +3,8 @@
 #   bash tools/gpu_round2.sh A TAG   -m gpu suite, smoke, c4 counters + kernel stats, the
 #                                    default bench line (CPU baselines), N=2 rehearsal
 #   bash tools/gpu_round2.sh B TAG   c3 and c5 counters + bench lines
+#   bash tools/gpu_round2.sh C TAG   c4 counters of rank 0 of 2, 4 and 8 (bench.py
+#                                    --profile-rank): the N-rank lines' issue roofline
 # Every GPU step has its own time limit; a failing step ends the script. The counter
 # summaries are written to gpurun_out/TAG/ (and into this copy's profiles/, so the bench
 # lines that follow carry the issue roofline).
@@ -27,6 +29,11 @@ if [ "$PART" = A ]; then
   YRT_BENCH_DEVICES=1 YRT_BENCH_BACKEND=gloo YRT_BENCH_OVERLAP=1 run timeout -k 10 400 \
     python bench.py --gpus 2 --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/bench_n2_rehearsal_gloo_1gpu.json 2> $OUT/n2.err
   grep -h '^{' $OUT/bench_n2_rehearsal_gloo_1gpu.json | cut -c1-300
+elif [ "$PART" = C ]; then
+  for n in 2 4 8; do
+    run bash tools/gpu_issue_pmc.sh $TAG/pmc_c4_r0of$n --profile-rank 0/$n > $OUT/pmc_c4_r0of$n.log 2>&1
+    summ instance10000-1920x1080-s8-n$n-wavefront $OUT/pmc_c4_r0of$n
+  done
 else
   PMC_TIMEOUT=200 run bash tools/gpu_issue_pmc.sh $TAG/pmc_c3 --scene refl --resolution 1080 --samples 4 > $OUT/pmc_c3.log 2>&1
   summ refl-1920x1080-s4-n1-wavefront $OUT/pmc_c3

@@ -476,6 +476,13 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #ifndef YRT_SHADOW_PERSIST
 #define YRT_SHADOW_PERSIST 2  // 0: one block per item; 1: fixed interleave (A/B +21 %); 2: per-XCD queue (A/B -1.9 %)
 #endif
+#ifndef YRT_SHADOW_PERSIST_MIN_ITEMS
+// the persistent grid pays a tail (its waves' last batches) that the hardware's block
+// dealing does not; it wins only with enough items per wave (A/B, items = 64-sample
+// blocks x lights: 6.2 M (a c4 frame) -1.9 %; 3.1 M (rank 0 of 2) +1.1 %; 1.6 M +5 %;
+// 0.8 M (rank 0 of 8) +16 %)
+#define YRT_SHADOW_PERSIST_MIN_ITEMS 4500000
+#endif
 #ifndef YRT_SHADOW_PERSIST_LEVELS
 #define YRT_SHADOW_PERSIST_LEVELS 0  // the persistent shadow kernel for the mirror levels too (A/B at c3: shadow +32 %)
 #endif
@@ -530,7 +537,8 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         return v;
     };
     // YRT_SHADOW_GRAB consecutive positions per atomic (one counter per XCD serialises:
-    // ~11 M atomics/s per address)
+    // ~11 M atomics/s per address; taking single positions near the end of the sequence
+    // contends there and loses, A/B: full frame +1.5 %, an eighth of it +11 %)
     constexpr unsigned G = YRT_SHADOW_GRAB;
     unsigned qv = YRT_SHADOW_PERSIST == 2 ? issue() : 0u;  // next batch, lane 0
     unsigned qb = 0, qleft = 0;                            // current batch (uniform)
@@ -545,8 +553,8 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
                 qleft = G;
                 qv = issue();
             }
-            q = qb++;
             qleft--;
+            q = qb++;
         } else {
             q = qj;
             qj += waves_xcd;
@@ -994,14 +1002,21 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     // per-level buffers for every level (~100 B per sample and level). The chunk is
     // halved until the workspace takes at most half of the free HBM.
     long long target = ds.reflective ? (1ll << 25) : (1ll << YRT_CHUNK_LOG2);
-    {
+    auto cap_for = [&](long long tgt) {
+        int pix = (int)std::max<long long>(1, std::min<long long>(npix_total, tgt / spp));
+        pix = ((pix + TILE * TILE - 1) / (TILE * TILE)) * TILE * TILE;
+        return pix;
+    };
+    int pix_per_chunk = cap_for(target);
+    // the free-memory query (a driver round trip) only when the workspace must grow: a
+    // steady frame loop reuses the workspace it already has
+    if (workspace_bytes(pix_per_chunk * spp, ds.nlights, nlevels) > ds.work_bytes) {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         free_b += ds.work_bytes;  // the current workspace is given back if it is regrown
         while (target > (1ll << 20) && workspace_bytes((int)target, ds.nlights, nlevels) > free_b / 2) target /= 2;
+        pix_per_chunk = cap_for(target);
     }
-    int pix_per_chunk = (int)std::max<long long>(1, std::min<long long>(npix_total, target / spp));
-    pix_per_chunk = ((pix_per_chunk + TILE * TILE - 1) / (TILE * TILE)) * TILE * TILE;
     const int cap = pix_per_chunk * spp;
     const size_t need = workspace_bytes(cap, ds.nlights, nlevels);
     if (need > ds.work_bytes) {
@@ -1077,7 +1092,8 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                     hipLaunchKernelGGL(k_shadow_dual, dim3(nb), dim3(SD_BLOCK), 0, stream, ds.view, nsamp, tgrid, B,
                                        counters);
                 } else if (YRT_SHADOW_PERSIST && !COUNT && PACKET && ds.wide_ok && TB == 64 &&
-                           (level == 0 || YRT_SHADOW_PERSIST_LEVELS)) {
+                           (level == 0 || YRT_SHADOW_PERSIST_LEVELS) &&
+                           (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS) {
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
                     if (YRT_SHADOW_PERSIST == 2) {
