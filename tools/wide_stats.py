@@ -1,0 +1,50 @@
+"""Diagnostic: per-walk work of the wide any-hit walk from a YRT_WIDE_STATS build
+(every shadow walk of one 64-ray wave adds its counts).
+
+    python tools/build_variants.py ws:-DYRT_WIDE_STATS
+    python tools/wide_stats.py yocto_raytracing_amd/variants/libyrt_ws.so [scene res s]
+"""
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tools"))
+sys.path.insert(0, str(ROOT))
+from ab_variants import bind  # noqa: E402
+
+import torch  # noqa: E402
+
+NAMES = ["walks", "steps_top", "steps_shape", "inst_entries", "leaves", "prim_tests", "pops", "empty_pops"]
+
+
+def main():
+    lib, N = bind(sys.argv[1])
+    name, res, s = (sys.argv[2], int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else ("instance10000", 1080, 8)
+    lib.yrt_debug_wide_stats.argtypes = [C.c_void_p, C.c_int]
+    torch.cuda.set_device(0)
+    hs, ds = C.c_void_p(), C.c_void_p()
+    scene = str(ROOT / "tests" / "golden" / "scenes" / f"{name}.yrtscene").encode()
+    assert lib.yrt_scene_load(scene, C.byref(hs)) == 0
+    assert lib.yrt_host_scene_build_bvh(hs, 0) == 0
+    assert lib.yrt_scene_upload(hs, 0, C.byref(ds)) == 0
+    p = N.RenderParams()
+    lib.yrt_render_params_default(C.byref(p))
+    p.resolution, p.samples = res, s
+    w, h = C.c_int(), C.c_int()
+    lib.yrt_image_size(ds, C.byref(p), C.byref(w), C.byref(h))
+    out = torch.empty((h.value, w.value, 4), dtype=torch.float32, device="cuda")
+    st = (C.c_ulonglong * 8)()
+    lib.yrt_debug_wide_stats(st, 1)
+    rc = lib.yrt_render(ds, C.byref(p), C.c_void_p(out.data_ptr()), 1, None)
+    torch.cuda.synchronize()
+    lib.yrt_debug_wide_stats(st, 1)
+    v = dict(zip(NAMES, list(st)))
+    walks = max(1, v["walks"])
+    print(json.dumps({"scene": name, "res": res, "s": s, "rc": rc, "totals": v,
+                      "per_walk": {k: round(x / walks, 2) for k, x in v.items()}}))
+
+
+if __name__ == "__main__":
+    main()

@@ -456,6 +456,16 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 #define DBG_CHECK(cond, code, a, b, c, d, e)
 #endif
 
+#ifdef YRT_WIDE_STATS
+// diagnostic build: per-wave work of the wide any-hit walk, summed over 1024 spread
+// lines of 8 counters: {walks, steps at the instance level, steps in shapes, instance
+// entries, leaves reached in shapes, primitive tests, pops, empty pops}
+static __device__ unsigned long long g_wide_stats[1024 * 8];
+#define WSTAT(i, v) (ws[i] += (v))
+#else
+#define WSTAT(i, v) ((void)0)
+#endif
+
 #ifndef YRT_FAST_DIV
 #define YRT_FAST_DIV 1
 #endif
@@ -898,26 +908,24 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #ifndef YRT_WIDE_SWITCH
 #define YRT_WIDE_SWITCH 0  // any hit: the passing children pushed by one switch on their 4-bit pattern (A/B: shadow +2.2 %; the switch compiles to a compare tree)
 #endif
+#ifndef YRT_WIDE_PUSHALL
+#define YRT_WIDE_PUSHALL 0  // wide step: every slot written to the stack, sp advanced per passing slot, top popped (A/B: shadow +6.8 %)
+#endif
 #ifndef YRT_WIDE_SKIP
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
 
-// one step of the 4-wide any-hit descent on the record r (in SGPRs when it came through
-// the scalar cache, in VGPRs -- the same value in every lane -- when it came from LDS):
-// the four slab tests, then the first passing child becomes current and the other
-// passing ones are pushed last-to-first (three v_writelane each: word, mask halves), so
-// they pop in slot order. Returns true to continue the descent from `cur`.
+// the slab tests of a wide step on the record r: m[k] = the lanes of `mask` that pass
+// slot k's box (0 for a slot the node does not have), w[k] = slot k's child word
 template <int OCT>
-__device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f ci, float tmin, float tmax,
-                                          uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
-                                          int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
+__device__ __forceinline__ void wide_tests(const float4 (&r)[8], vec3f co, vec3f ci, float tmin, float tmax,
+                                           unsigned long long mask, uint32_t (&w)[4], unsigned long long (&m)[4]) {
     const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
                 lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
                 hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
-    const uint32_t w[4] = {(uint32_t)uniform(ibits(r[6].x)), (uint32_t)uniform(ibits(r[6].y)),
-                           (uint32_t)uniform(ibits(r[6].z)), (uint32_t)uniform(ibits(r[6].w))};
+    w[0] = (uint32_t)uniform(ibits(r[6].x)), w[1] = (uint32_t)uniform(ibits(r[6].y));
+    w[2] = (uint32_t)uniform(ibits(r[6].z)), w[3] = (uint32_t)uniform(ibits(r[6].w));
     const int nslots = uniform(ibits(r[7].x));
-    unsigned long long m[4];
     if constexpr (YRT_PK_BOX && OCT < 8) {
         // slots 0 and 1 always (a leaf root's empty slot 1 fails its test), 2 and 3
         // when the node has a third slot; a missing fourth is masked out
@@ -943,6 +951,20 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
                 m[k] = 0;
         }
     }
+}
+
+// one step of the 4-wide any-hit descent on the record r (in SGPRs when it came through
+// the scalar cache, in VGPRs -- the same value in every lane -- when it came from LDS):
+// the four slab tests, then the first passing child becomes current and the other
+// passing ones are pushed last-to-first (three v_writelane each: word, mask halves), so
+// they pop in slot order. Returns true to continue the descent from `cur`.
+template <int OCT>
+__device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f ci, float tmin, float tmax,
+                                          uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
+                                          int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
+    uint32_t w[4];
+    unsigned long long m[4];
+    wide_tests<OCT>(r, co, ci, tmin, tmax, mask, w, m);
     unsigned long long cm = 0;
     uint32_t cw = 0;
 #if YRT_WIDE_SWITCH
@@ -1030,10 +1052,81 @@ template <int OCT, int LDSN>
 __device__ __forceinline__ void wide_descend(const dev_scene_view& S, const float4* lds, vec3f co, vec3f ci,
                                              float tmin, float tmax, uint32_t& cur, unsigned long long& mask,
                                              int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
-                                             unsigned long long done) {
+                                             unsigned long long done, unsigned& nsteps) {
     const f4* wbase = sgpr_ptr(S.wnodes);
+#if YRT_WIDE_PUSHALL
+    // every slot is written to stack lane sp, highest first, and sp advances past each
+    // one with live lanes (s_cmp_lg_u64 + s_addc_u32, no branch per slot); then the top
+    // entry is popped: the lowest passing slot if any passed (it pops first, as the
+    // select chain's current item would), else the entry below -- the pop the walk makes
+    // next anyway. One asm block: M0 carries sp (a v_writelane takes its lane select from
+    // M0 so that the data SGPR is its one constant-bus read). Absent slots have m = 0.
+    for (;;) {
+#ifdef YRT_WIDE_STATS
+        nsteps++;
+#endif
+        float4 r[8];
+        if (LDSN > 0 && cur < (uint32_t)(LDSN * wide_record_bytes)) {
+            const float4* p = lds + (cur >> 4);
+#pragma unroll
+            for (int k = 0; k < 8; k++) r[k] = p[k];
+        } else {
+            sgpr16 a, b;
+            asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(a), "=&s"(b)
+                         : "s"(wbase), "s"(uniform((int)cur)));
+#pragma unroll
+            for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
+        }
+        uint32_t w[4];
+        unsigned long long m[4];
+        wide_tests<OCT>(r, co, ci, tmin, tmax, mask, w, m);
+        int spn;
+        uint32_t cw, ml, mh;
+        asm volatile(
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w3], m0\n v_writelane_b32 %[sl], %[l3], m0\n v_writelane_b32 %[sh], %[h3], m0\n"
+            "s_cmp_lg_u64 %[m3], 0\n s_addc_u32 m0, m0, 0\n"
+            "v_writelane_b32 %[sw], %[w2], m0\n v_writelane_b32 %[sl], %[l2], m0\n v_writelane_b32 %[sh], %[h2], m0\n"
+            "s_cmp_lg_u64 %[m2], 0\n s_addc_u32 m0, m0, 0\n"
+            "v_writelane_b32 %[sw], %[w1], m0\n v_writelane_b32 %[sl], %[l1], m0\n v_writelane_b32 %[sh], %[h1], m0\n"
+            "s_cmp_lg_u64 %[m1], 0\n s_addc_u32 m0, m0, 0\n"
+            "v_writelane_b32 %[sw], %[w0], m0\n v_writelane_b32 %[sl], %[l0], m0\n v_writelane_b32 %[sh], %[h0], m0\n"
+            "s_cmp_lg_u64 %[m0], 0\n s_addc_u32 m0, m0, 0\n"
+            "s_sub_u32 m0, m0, 1\n"
+            "v_readlane_b32 %[cw], %[sw], m0\n v_readlane_b32 %[ml], %[sl], m0\n v_readlane_b32 %[mh], %[sh], m0\n"
+            "s_mov_b32 %[spn], m0"
+            : [spn] "=&s"(spn), [cw] "=&s"(cw), [ml] "=&s"(ml), [mh] "=&s"(mh), [sw] "+v"(stk_word),
+              [sl] "+v"(stk_mlo), [sh] "+v"(stk_mhi)
+            : [sp] "s"(sp), [w0] "s"(w[0]), [w1] "s"(w[1]), [w2] "s"(w[2]), [w3] "s"(w[3]), [m0] "s"(m[0]),
+              [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3]), [l0] "s"((uint32_t)m[0]), [l1] "s"((uint32_t)m[1]),
+              [l2] "s"((uint32_t)m[2]), [l3] "s"((uint32_t)m[3]), [h0] "s"((uint32_t)(m[0] >> 32)),
+              [h1] "s"((uint32_t)(m[1] >> 32)), [h2] "s"((uint32_t)(m[2] >> 32)), [h3] "s"((uint32_t)(m[3] >> 32))
+            : "m0", "scc");
+        // asm results count as divergent to the compiler: readfirstlane (folded away on
+        // SGPRs) tells it they are wave-uniform, so what follows stays on the scalar unit
+        spn = uniform(spn);
+        if (spn < floor) {  // nothing passed and nothing left above the floor
+            sp = floor;
+            mask = 0;
+            return;
+        }
+        sp = spn;
+        cur = (uint32_t)uniform((int)cw);
+        mask = ((unsigned long long)(uint32_t)uniform((int)mh) << 32 | (uint32_t)uniform((int)ml)) & ~done;
+        if (!mask) {
+            int n = 0;
+            if (!inner_pop(floor, done, n, mask, sp, stk_word, stk_mlo, stk_mhi)) return;
+            cur = (uint32_t)n;
+        }
+        if (cur & wide_leaf) return;
+    }
+#endif
     for (;;) {
         bool more;
+#ifdef YRT_WIDE_STATS
+        nsteps++;
+#endif
         if (LDSN > 0 && cur < (uint32_t)(LDSN * wide_record_bytes)) {
             float4 r[8];
             const float4* p = lds + (cur >> 4);
@@ -1081,13 +1174,18 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     // the octant of the current level's rays when the whole wave shares it (8: mixed)
     const int woct = YRT_WIDE_OCTANT ? wave_octant(wi, live) : 8;
     int oct = woct;
+    unsigned nsteps0 = 0, nsteps1 = 0;
+#ifdef YRT_WIDE_STATS
+    unsigned ws[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+#endif
     for (;;) {
         // ---- descent through wide nodes until a leaf or no passing child ----
         if (!(cur & wide_leaf)) {
             const int wfloor = level ? base : 0;
             DBG_CHECK(cur < (uint32_t)S.nwnodes * wide_record_bytes && sp >= 0 && sp < 61, 4, (int)cur, sp, level,
                       base, 0);
-#define YRT_WD(o) wide_descend<o, LDSN>(S, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done)
+#define YRT_WD(o) wide_descend<o, LDSN>(S, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done, \
+                                         level ? nsteps1 : nsteps0)
 #if YRT_WIDE_OCTANT
             switch (oct) {
                 case 0: YRT_WD(0); break;
@@ -1119,6 +1217,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 DBG_CHECK(first >= 0 && first + count <= S.nsprims, 5, first, count, level, kind, sp);
                 const bool inl = (mask & me) != 0;
                 int leaf_hit = 0;
+                WSTAT(4, 1u);
+                WSTAT(5, (unsigned)count);
                 if (kind == kind_triangles) {
                     for (int i = first; i < first + count; i++) {
                         float4 pv[3];
@@ -1164,6 +1264,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
                     mask = inst_mask & ~done;
+                    WSTAT(3, 1u);
                     if (YRT_WIDE_OCTANT) oct = wave_octant(ci, live & ~done);
                     if (mask) break;
                     continue;
@@ -1183,10 +1284,19 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
                     (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
                    ~done;
+            WSTAT(6, 1u);
+            WSTAT(7, mask ? 0u : 1u);
             if (mask) break;
         }
         if (finished) break;
     }
+#ifdef YRT_WIDE_STATS
+    ws[1] = nsteps0, ws[2] = nsteps1;
+    if (__lane_id() == 0) {
+        unsigned long long* line = g_wide_stats + 8 * ((blockIdx.x * 7u + threadIdx.x / 64u) & 1023u);
+        for (int i = 0; i < 8; i++) atomicAdd(line + i, (unsigned long long)ws[i]);
+    }
+#endif
     return (done & me) != 0;
 }
 
