@@ -16,7 +16,8 @@ from ab_variants import bind  # noqa: E402
 
 import torch  # noqa: E402
 
-NAMES = ["walks", "steps_top", "steps_shape", "inst_entries", "leaves", "prim_tests", "pops", "empty_pops"]
+NAMES = ["walks", "steps_top", "steps_shape", "inst_entries", "leaves", "prim_tests", "pops", "empty_pops",
+         "live_lanes", "occluded_lanes", "walks_all_occluded", "steps_in_all_occluded", "-", "-", "-", "-"]
 
 
 def main():
@@ -35,12 +36,12 @@ def main():
     w, h = C.c_int(), C.c_int()
     lib.yrt_image_size(ds, C.byref(p), C.byref(w), C.byref(h))
     out = torch.empty((h.value, w.value, 4), dtype=torch.float32, device="cuda")
-    st = (C.c_ulonglong * 8)()
+    st = (C.c_ulonglong * 16)()
     lib.yrt_debug_wide_stats(st, 1)
     rc = lib.yrt_render(ds, C.byref(p), C.c_void_p(out.data_ptr()), 1, None)
     torch.cuda.synchronize()
     lib.yrt_debug_wide_stats(st, 1)
-    v = dict(zip(NAMES, list(st)))
+    v = {k: x for k, x in zip(NAMES, list(st)) if k != "-"}
     walks = max(1, v["walks"])
     print(json.dumps({"scene": name, "res": res, "s": s, "rc": rc, "totals": v,
                       "per_walk": {k: round(x / walks, 2) for k, x in v.items()}}))

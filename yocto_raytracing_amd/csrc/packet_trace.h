@@ -458,9 +458,10 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 
 #ifdef YRT_WIDE_STATS
 // diagnostic build: per-wave work of the wide any-hit walk, summed over 1024 spread
-// lines of 8 counters: {walks, steps at the instance level, steps in shapes, instance
-// entries, leaves reached in shapes, primitive tests, pops, empty pops}
-static __device__ unsigned long long g_wide_stats[1024 * 8];
+// lines of 16 counters: {walks, steps at the instance level, steps in shapes, instance
+// entries, leaves reached in shapes, primitive tests, pops, empty pops, live lanes,
+// occluded lanes, walks that end with every live lane occluded, their steps}
+static __device__ unsigned long long g_wide_stats[1024 * 16];
 #define WSTAT(i, v) (ws[i] += (v))
 #else
 #define WSTAT(i, v) ((void)0)
@@ -1176,7 +1177,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     int oct = woct;
     unsigned nsteps0 = 0, nsteps1 = 0;
 #ifdef YRT_WIDE_STATS
-    unsigned ws[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    unsigned ws[16] = {1, 0, 0, 0, 0, 0, 0, 0};
 #endif
     for (;;) {
         // ---- descent through wide nodes until a leaf or no passing child ----
@@ -1292,9 +1293,11 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     }
 #ifdef YRT_WIDE_STATS
     ws[1] = nsteps0, ws[2] = nsteps1;
+    ws[8] = (unsigned)__popcll(live), ws[9] = (unsigned)__popcll(done & live);
+    ws[10] = (live & ~done) ? 0u : 1u, ws[11] = (live & ~done) ? 0u : nsteps0 + nsteps1;
     if (__lane_id() == 0) {
-        unsigned long long* line = g_wide_stats + 8 * ((blockIdx.x * 7u + threadIdx.x / 64u) & 1023u);
-        for (int i = 0; i < 8; i++) atomicAdd(line + i, (unsigned long long)ws[i]);
+        unsigned long long* line = g_wide_stats + 16 * ((blockIdx.x * 7u + threadIdx.x / 64u) & 1023u);
+        for (int i = 0; i < 12; i++) atomicAdd(line + i, (unsigned long long)ws[i]);
     }
 #endif
     return (done & me) != 0;

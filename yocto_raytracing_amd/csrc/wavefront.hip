@@ -1173,15 +1173,15 @@ hipError_t launch_render_wavefront(device_scene& ds, const dev_render_args& args
 }  // namespace yrt
 
 #ifdef YRT_WIDE_STATS
-extern "C" int yrt_debug_wide_stats(unsigned long long* out8, int reset) {
-    static unsigned long long h[1024 * 8];
+extern "C" int yrt_debug_wide_stats(unsigned long long* out16, int reset) {
+    static unsigned long long h[1024 * 16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(yrt::g_wide_stats), sizeof h) != hipSuccess) return -1;
-    for (int i = 0; i < 8; i++) {
-        out8[i] = 0;
-        for (int k = 0; k < 1024; k++) out8[i] += h[8 * k + i];
+    for (int i = 0; i < 16; i++) {
+        out16[i] = 0;
+        for (int k = 0; k < 1024; k++) out16[i] += h[16 * k + i];
     }
     if (reset) {
-        static const unsigned long long z[1024 * 8] = {};
+        static const unsigned long long z[1024 * 16] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_wide_stats), z, sizeof z);
     }
     return 0;
