@@ -14,7 +14,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 run() { "$@"; local rc=$?; if [ $rc -ne 0 ]; then echo "FAILED (rc=$rc): $*"; exit $rc; fi; }
 summ() {  # key, pmc dir
-  run python tools/pmc_summary.py --key $1 --csv $2/p*/p*_counter_collection.csv --source profiles/r2/$TAG \
+  run python tools/pmc_summary.py --key $1 --csv $2/p*/p*_counter_collection.csv --source profiles/r2/${2#gpurun_out/} \
       --traffic profiles/pmc_traffic.json --issue profiles/issue_counters.json > $2/summary.json
   cp profiles/pmc_traffic.json profiles/issue_counters.json $OUT/
 }
