@@ -631,6 +631,9 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
 #endif
 constexpr int packet_block = 256;  // >= threads per block of every kernel that runs packet_first
 
+#ifndef YRT_FIRST_HOIST
+#define YRT_FIRST_HOIST 1  // closest-hit descent: the record base made wave-uniform once per descent
+#endif
 #ifndef YRT_FIRST_OCTANT
 #define YRT_FIRST_OCTANT 1  // closest hit: octant-specialised slab tests (see box_oct)
 #endif
@@ -645,20 +648,25 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
                                               work_counts& wc, int floor, unsigned long long done) {
     constexpr bool FILTER = YRT_FIRST_FILTER && !COUNT;  // the instrumented pass counts the reference's tests
+#if YRT_FIRST_HOIST
+    const f4* pb = sgpr_ptr(pbase);  // once per descent, not per record (the compiler kept pbase in VGPRs)
+#else
+#define pb sgpr_ptr(pbase)
+#endif
     for (;;) {
         float4 rec[FILTER ? 8 : 4];
         if constexpr (FILTER) {
             sgpr16 a, b;
             asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
                          : "=&s"(a), "=&s"(b)
-                         : "s"(sgpr_ptr(pbase)), "s"(uniform(node)));
+                         : "s"(pb), "s"(uniform(node)));
 #pragma unroll
             for (int k = 0; k < 4; k++) rec[k] = rec_of(a, k), rec[4 + k] = rec_of(b, k);
         } else {
             sgpr16 a;
             asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
                          : "=s"(a)
-                         : "s"(sgpr_ptr(pbase)), "s"(uniform(node)));
+                         : "s"(pb), "s"(uniform(node)));
             rec[0] = rec_of(a, 0), rec[1] = rec_of(a, 1), rec[2] = rec_of(a, 2), rec[3] = rec_of(a, 3);
         }
         bool p0, p1;
@@ -727,6 +735,9 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         }
         node = s1 + spine_record_bytes;
     }
+#if !YRT_FIRST_HOIST
+#undef pb
+#endif
 }
 
 // ---- closest hit, laid out for the scalar unit ----
