@@ -923,6 +923,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #ifndef YRT_WIDE_PUSHALL
 #define YRT_WIDE_PUSHALL 0  // wide step: every slot written to the stack, sp advanced per passing slot, top popped (A/B: shadow +6.8 %)
 #endif
+#ifndef YRT_WIDE_ASMSEL
+#define YRT_WIDE_ASMSEL 1  // wide step: the passing-slot selection and pushes as one scalar asm block
+#endif
 #ifndef YRT_WIDE_SKIP
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
@@ -1007,6 +1010,112 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
         case 14: push(3, 0); push(2, 1); sp += 2; cm = m[1]; cw = w[1]; break;
         case 15: push(3, 0); push(2, 1); push(1, 2); sp += 3; cm = m[0]; cw = w[0]; break;
         default: break;
+    }
+#elif YRT_WIDE_ASMSEL
+    // the select chain as written for the scalar unit. Chain A tests the slots from the
+    // highest while none has passed; the first passing slot j becomes the candidate and
+    // control moves to the blocks that know it: B(j,k) tests slot k < j and, when it
+    // passes, pushes slot j's word and mask halves straight from the record/ballot
+    // registers (three v_writelane at lane sp) and continues in B(k, k-1). FIN(j) hands
+    // back slot j. Per slot one s_cmp_lg_u64 and one branch; no materialised conditions
+    // and no copies of the candidate. cm = 0 when no slot passed.
+    {
+        uint32_t ow;
+        unsigned long long om;
+        asm volatile(
+            "s_cmp_lg_u64 %[m3], 0\n"
+            "s_cbranch_scc1 .Lyb32_%=\n"
+            "s_cmp_lg_u64 %[m2], 0\n"
+            "s_cbranch_scc1 .Lyb21_%=\n"
+            "s_cmp_lg_u64 %[m1], 0\n"
+            "s_cbranch_scc1 .Lyb10_%=\n"
+            "s_cmp_lg_u64 %[m0], 0\n"
+            "s_cbranch_scc1 .Lyfin0_%=\n"
+            "s_mov_b64 %[cm], 0\n"
+            "s_mov_b32 %[cw], 0\n"
+            "s_branch .Lyend_%=\n"
+            ".Lyb32_%=:\n"
+            "s_cmp_lg_u64 %[m2], 0\n"
+            "s_cbranch_scc0 .Lyb31_%=\n"
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w3], m0\n"
+            "v_writelane_b32 %[sl], %[l3], m0\n"
+            "v_writelane_b32 %[sh], %[h3], m0\n"
+            "s_add_u32 %[sp], %[sp], 1\n"
+            "s_branch .Lyb21_%=\n"
+            ".Lyb31_%=:\n"
+            "s_cmp_lg_u64 %[m1], 0\n"
+            "s_cbranch_scc0 .Lyb30_%=\n"
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w3], m0\n"
+            "v_writelane_b32 %[sl], %[l3], m0\n"
+            "v_writelane_b32 %[sh], %[h3], m0\n"
+            "s_add_u32 %[sp], %[sp], 1\n"
+            "s_branch .Lyb10_%=\n"
+            ".Lyb30_%=:\n"
+            "s_cmp_lg_u64 %[m0], 0\n"
+            "s_cbranch_scc0 .Lyfin3_%=\n"
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w3], m0\n"
+            "v_writelane_b32 %[sl], %[l3], m0\n"
+            "v_writelane_b32 %[sh], %[h3], m0\n"
+            "s_add_u32 %[sp], %[sp], 1\n"
+            "s_branch .Lyfin0_%=\n"
+            ".Lyb21_%=:\n"
+            "s_cmp_lg_u64 %[m1], 0\n"
+            "s_cbranch_scc0 .Lyb20_%=\n"
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w2], m0\n"
+            "v_writelane_b32 %[sl], %[l2], m0\n"
+            "v_writelane_b32 %[sh], %[h2], m0\n"
+            "s_add_u32 %[sp], %[sp], 1\n"
+            "s_branch .Lyb10_%=\n"
+            ".Lyb20_%=:\n"
+            "s_cmp_lg_u64 %[m0], 0\n"
+            "s_cbranch_scc0 .Lyfin2_%=\n"
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w2], m0\n"
+            "v_writelane_b32 %[sl], %[l2], m0\n"
+            "v_writelane_b32 %[sh], %[h2], m0\n"
+            "s_add_u32 %[sp], %[sp], 1\n"
+            "s_branch .Lyfin0_%=\n"
+            ".Lyb10_%=:\n"
+            "s_cmp_lg_u64 %[m0], 0\n"
+            "s_cbranch_scc0 .Lyfin1_%=\n"
+            "s_mov_b32 m0, %[sp]\n"
+            "v_writelane_b32 %[sw], %[w1], m0\n"
+            "v_writelane_b32 %[sl], %[l1], m0\n"
+            "v_writelane_b32 %[sh], %[h1], m0\n"
+            "s_add_u32 %[sp], %[sp], 1\n"
+            "s_branch .Lyfin0_%=\n"
+            ".Lyfin3_%=:\n"
+            "s_mov_b32 %[cw], %[w3]\n"
+            "s_mov_b64 %[cm], %[m3]\n"
+            "s_branch .Lyend_%=\n"
+            ".Lyfin2_%=:\n"
+            "s_mov_b32 %[cw], %[w2]\n"
+            "s_mov_b64 %[cm], %[m2]\n"
+            "s_branch .Lyend_%=\n"
+            ".Lyfin1_%=:\n"
+            "s_mov_b32 %[cw], %[w1]\n"
+            "s_mov_b64 %[cm], %[m1]\n"
+            "s_branch .Lyend_%=\n"
+            ".Lyfin0_%=:\n"
+            "s_mov_b32 %[cw], %[w0]\n"
+            "s_mov_b64 %[cm], %[m0]\n"
+            ".Lyend_%=:\n"
+            : [cw] "=&s"(ow), [cm] "=&s"(om), [sp] "+s"(sp), [sw] "+v"(stk_word), [sl] "+v"(stk_mlo),
+              [sh] "+v"(stk_mhi)
+            : [w0] "s"(w[0]), [w1] "s"(w[1]), [w2] "s"(w[2]), [w3] "s"(w[3]), [m0] "s"(m[0]), [m1] "s"(m[1]),
+              [m2] "s"(m[2]), [m3] "s"(m[3]), [l0] "s"((uint32_t)m[0]), [l1] "s"((uint32_t)m[1]),
+              [l2] "s"((uint32_t)m[2]), [l3] "s"((uint32_t)m[3]), [h0] "s"((uint32_t)(m[0] >> 32)),
+              [h1] "s"((uint32_t)(m[1] >> 32)), [h2] "s"((uint32_t)(m[2] >> 32)), [h3] "s"((uint32_t)(m[3] >> 32))
+            : "m0", "scc");
+        // asm results count as divergent to the compiler: readfirstlane (folded away on
+        // SGPRs) keeps what follows on the scalar unit
+        sp = uniform(sp);
+        cw = (uint32_t)uniform((int)ow);
+        cm = (unsigned long long)(uint32_t)uniform((int)(om >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)om);
     }
 #else
 #pragma unroll
