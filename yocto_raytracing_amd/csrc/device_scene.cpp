@@ -187,8 +187,30 @@ struct wide_builder {
     std::vector<int> slots_of(const bvh_tree& t, int x) const {
         std::vector<int> slots;
         const bvh_node& n = t.nodes[x];
+        auto area = [&](int i) {
+            const bbox3f& b = t.nodes[i].bbox;
+            const vec3f d = b.max - b.min;
+            return d.x * d.y + d.y * d.z + d.z * d.x;
+        };
+#ifndef YRT_WIDE_GREEDY
+#define YRT_WIDE_GREEDY 0  // largest-area-first collapse (A/B: instance-level steps 7.06 -> 6.76 per walk, shadow time unchanged)
+#endif
         if (n.isleaf) {
             slots.push_back(x);
+        } else if (YRT_WIDE_GREEDY) {
+            // x's two children, then while there is room the inner slot with the largest
+            // surface area is replaced by its two children (the slot most rays reach is
+            // opened first): up to four slots whichever levels they come from
+            slots = {(int)n.start + 1, (int)n.start};
+            while (slots.size() < 4) {
+                int best = -1;
+                for (int k = 0; k < (int)slots.size(); k++)
+                    if (!t.nodes[slots[k]].isleaf && (best < 0 || area(slots[k]) > area(slots[best]))) best = k;
+                if (best < 0) break;
+                const bvh_node& cn = t.nodes[slots[best]];
+                slots[best] = (int)cn.start + 1;
+                slots.insert(slots.begin() + best + 1, (int)cn.start);
+            }
         } else {
             for (int c : {(int)n.start + 1, (int)n.start}) {  // the reference visits start+1 first
                 const bvh_node& cn = t.nodes[c];
@@ -206,11 +228,6 @@ struct wide_builder {
 #ifndef YRT_WIDE_SORT
 #define YRT_WIDE_SORT -1
 #endif
-        auto area = [&](int i) {
-            const bbox3f& b = t.nodes[i].bbox;
-            const vec3f d = b.max - b.min;
-            return d.x * d.y + d.y * d.z + d.z * d.x;
-        };
         if (YRT_WIDE_SORT == 3)  // lowest first (experiment: up-going shadow rays)
             std::stable_sort(slots.begin(), slots.end(),
                              [&](int a, int b) { return t.nodes[a].bbox.min.y < t.nodes[b].bbox.min.y; });
