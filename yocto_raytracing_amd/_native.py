@@ -17,6 +17,20 @@ if not LIB_PATH.exists():
         f"{LIB_PATH} not found: build it with `python yocto_raytracing_amd/build.py` "
         "(or __graft_entry__.build()); there is no fallback path")
 
+# One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64 (SONAME
+# libamdhip64.so.7, but torch asks for it as "libamdhip64.so"): if libyrt.so is loaded
+# first, /opt/rocm's runtime is mapped, torch then maps its bundled copy on top of the
+# same HSA runtime and finds no GPU ("No HIP GPUs are available"). With torch loaded
+# first, libyrt.so's libamdhip64.so.7 resolves to torch's copy and both share it. torch
+# is plumbing here (device buffers, streams, torch.distributed), so when it is installed
+# it is imported before the library; YRT_NO_TORCH_PRELOAD=1 skips this for processes
+# that never import torch.
+if os.environ.get("YRT_NO_TORCH_PRELOAD") != "1":
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
 lib = C.CDLL(str(LIB_PATH))
 
 YRT_OK = 0
