@@ -480,7 +480,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     ds->wide_ok = 3 * (wtop_depth + wshape_depth) + 2 <= 64;
 
     // ---- instance level: nodes + instances permuted into leaf order ----
-    std::vector<f4> tnodes, tinst;
+    std::vector<f4> tnodes, tinst, winst;
     std::vector<int> tinst_id;
     for (auto& n : scn.bvh.nodes) {
         tnodes.push_back(node_lo(n, n.start));
@@ -569,6 +569,17 @@ device_scene* device_scene_create(const scene& scn, int device) {
         const i4 sh = shapes[ist.shp];
         if (sh.x >= (1 << 30)) throw unsupported_error("scene too large (shape nodes >= 2^30, unsupported)");
         tinst.push_back({f.o.x, f.o.y, f.o.z, as_float((int)((uint32_t)sh.x | ((uint32_t)sh.y << 30)))});
+        // any-hit copy with the shape's root box (an empty shape: a box no finite ray passes)
+        winst.insert(winst.end(), tinst.end() - 4, tinst.end());
+        const shape& sp = scn.shapes[ist.shp];
+        if (sp.bvh.nodes.empty()) {
+            winst.push_back({INFINITY, INFINITY, INFINITY, 0});
+            winst.push_back({-INFINITY, -INFINITY, -INFINITY, 0});
+        } else {
+            const bbox3f& rb = sp.bvh.nodes[0].bbox;
+            winst.push_back({rb.min.x, rb.min.y, rb.min.z, 0});
+            winst.push_back({rb.max.x, rb.max.y, rb.max.z, 0});
+        }
     }
 
     // ---- materials, lights, textures ----
@@ -632,6 +643,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_texinfo = ab.add(texinfo.data(), texinfo.size() * sizeof(i4));
     size_t o_srgb = ab.add(srgb.data(), srgb.size() * sizeof(float));
     size_t o_wnodes = ab.add(wnodes.data(), wnodes.size() * sizeof(f4));
+    size_t o_winst = ab.add(winst.data(), winst.size() * sizeof(f4));
     size_t o_tpair = ab.add(tpair.data(), tpair.size() * sizeof(f4));
     size_t o_spair = ab.add(spair.data(), spair.size() * sizeof(f4));
     size_t o_tinst_id = ab.add(tinst_id.data(), tinst_id.size() * sizeof(int));
@@ -673,6 +685,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.texinfo = (const i4*)(base + o_texinfo);
     v.srgb = (const float*)(base + o_srgb);
     v.wnodes = (const f4*)(base + o_wnodes);
+    v.winst = (const f4*)(base + o_winst);
     v.tpair = (const f4*)(base + o_tpair);
     v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);

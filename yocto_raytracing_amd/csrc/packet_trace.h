@@ -172,13 +172,21 @@ __device__ __forceinline__ void ld_records(const f4* p, float4 (&out)[N]) {
 // (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
 template <int N>
 __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
-    static_assert(N == 4 || N == 8, "record count");
+    static_assert(N == 4 || N == 6 || N == 8, "record count");
     const f4* base = sgpr_ptr(base_);
     const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
     if constexpr (N == 4) {
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+    } else if constexpr (N == 6) {
+        sgpr16 a;
+        sgpr8 b;
+        asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx8 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                     : "=&s"(a), "=&s"(b)
+                     : "s"(base), "s"(off));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+        out[4] = rec_of(b, 0), out[5] = rec_of(b, 1);
     } else {
         sgpr16 a, b;
         asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
@@ -196,7 +204,7 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
 template <int N>
 __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, float4 (&out)[N]) {
 #if YRT_SCALAR_LOADS && YRT_SOFF
-    if constexpr (N == 4 || N == 8) {
+    if constexpr (N == 4 || N == 6 || N == 8) {
         ld_scalar_at<N>(base, index, out);
         return;
     }
@@ -926,6 +934,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #ifndef YRT_WIDE_ASMSEL
 #define YRT_WIDE_ASMSEL 1  // wide step: the passing-slot selection and pushes as one scalar asm block
 #endif
+#ifndef YRT_WIDE_ROOTBOX
+#define YRT_WIDE_ROOTBOX 1  // any hit: a shape's root box tested on entering an instance
+#endif
 #ifndef YRT_WIDE_SKIP
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
@@ -1376,8 +1387,9 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 if (inst_next < inst_end) {
                     const int k = inst_next++;
                     DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_end, sp, base, 0);
-                    float4 fr[4];
-                    ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
+                    float4 fr[YRT_WIDE_ROOTBOX ? 6 : 4];
+                    constexpr int NR = YRT_WIDE_ROOTBOX ? 6 : 4;
+                    ld_records_at<NR>(YRT_WIDE_ROOTBOX ? S.winst : S.tinst, (unsigned)(NR * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
                     enter_direction(f, wd, live & ~done, cd, ci);
@@ -1385,6 +1397,15 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
                     mask = inst_mask & ~done;
+                    if constexpr (YRT_WIDE_ROOTBOX) {
+                        // the shape root's own box, which the wide root (its children's
+                        // children) skips: the reference tests it first, and a lane that
+                        // fails it finds nothing in this instance (every box below is
+                        // inside it)
+                        float tn;
+                        mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[4].x, fr[4].y, fr[4].z, fr[5].x, fr[5].y,
+                                                fr[5].z, tn));
+                    }
                     WSTAT(3, 1u);
                     if (YRT_WIDE_OCTANT) oct = wave_octant(ci, live & ~done);
                     if (mask) break;

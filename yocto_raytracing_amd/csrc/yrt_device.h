@@ -22,6 +22,9 @@
 //   wnodes  8 x f4 per 4-wide node of the any-hit walk (device_scene.cpp wide_builder):
 //           {lo.x[4]} {lo.y[4]} {lo.z[4]} {hi.x[4]} {hi.y[4]} {hi.z[4]} {ref[4]} {info[4]},
 //           instance level and all shapes in one array, absolute indices
+//   winst   6 x f4 per instance-BVH leaf slot for the any-hit walk: tinst's four rows, then
+//           the object-space root box of the instance's shape {lo, -} {hi, -} (the box the
+//           reference tests first on entering it, scene.cpp:386-442)
 #pragma once
 
 #include <stdint.h>
@@ -83,6 +86,7 @@ struct dev_scene_view {
     const i4* texinfo;
     const float* srgb;
     const f4* wnodes;
+    const f4* winst;
     const f4* tpair;  // 2*spine_len x f4 per instance-BVH node: its record, then its
                       // child start+1's, that child's start+1's, ... (right spine)
     const f4* spair;  // the same for the shape BVHs (same indexing as snodes)
