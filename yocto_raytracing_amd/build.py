@@ -37,7 +37,11 @@ LINK_LIBS = ["-lz", "-ldl", "-lpthread"]
 # device code: leave wave-uniform regions unstructurized. Every branch of the BVH walks
 # is on an SGPR value; structurizing them adds flow variables and exec-mask juggling
 # (SALU) to every traversal step (A/B at c4: primary -2 %, shadow -4 %).
-DEVICE_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=true"]
+DEVICE_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=true",
+                # no SLP packing of adjacent f32 adds/muls into v_pk_*_f32: packed f32 does
+                # not issue faster here and lengthens the dependent chains (A/B at c4:
+                # primary -3 %, shadow -6.7 %, frame 32.7 -> 31.1 ms; identical images)
+                "-fno-slp-vectorize"]
 
 
 def _headers():
