@@ -477,11 +477,12 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #define YRT_SHADOW_PERSIST 2  // 0: one block per item; 1: fixed interleave (A/B +21 %); 2: per-XCD queue (A/B -1.9 %)
 #endif
 #ifndef YRT_SHADOW_PERSIST_MIN_ITEMS
-// the persistent grid pays a tail (its waves' last batches) that the hardware's block
-// dealing does not; it wins only with enough items per wave (A/B, items = 64-sample
-// blocks x lights: 6.2 M (a c4 frame) -1.9 %; 3.1 M (rank 0 of 2) +1.1 %; 1.6 M +5 %;
-// 0.8 M (rank 0 of 8) +16 %)
-#define YRT_SHADOW_PERSIST_MIN_ITEMS 4500000
+// the persistent grid pays a tail (its waves' last batches, ~0.26 ms) that the hardware's
+// block dealing does not, and saves the dealing's per-block cost (~6 % of the walk time
+// since the walks got cheaper); it wins with enough items per wave (A/B, items = 64-sample
+// blocks x lights: 6.2 M (a c4 frame) -6 %; 3.1 M (rank 0 of 2) -3 %; 1.6 M +2 %;
+// 0.8 M (rank 0 of 8) +13 %)
+#define YRT_SHADOW_PERSIST_MIN_ITEMS 2000000
 #endif
 #ifndef YRT_SHADOW_PERSIST_LEVELS
 #define YRT_SHADOW_PERSIST_LEVELS 0  // the persistent shadow kernel for the mirror levels too (A/B at c3: shadow +32 %)
