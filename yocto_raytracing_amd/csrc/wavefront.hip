@@ -684,6 +684,9 @@ __global__ __launch_bounds__(SD_BLOCK, YRT_SHADOW_DUAL_WAVES) void k_shadow_dual
 #ifndef YRT_SHADE_OCC4
 #define YRT_SHADE_OCC4 1  // k_shade: occlusion bytes of <= 4 lights loaded with the surface
 #endif
+#ifndef YRT_SHADE_POW_FIRST
+#define YRT_SHADE_POW_FIRST 0  // k_shade: the specular powers in a pass of their own (A/B: c4 shade +22 %, c3 -5 %; VGPRs 95 natural)
+#endif
 #ifndef YRT_SHADE_WAVES
 #define YRT_SHADE_WAVES 5  // k_shade register budget (its natural 96 VGPRs; A/B: 6 -> +26 %, 8 -> +140 % from spills)
 #endif
@@ -694,6 +697,8 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
     const int n = level ? B.count[level] : nsamp_level0;
+    constexpr bool POWF = YRT_SHADE_POW_FIRST && OCC4;
+    __shared__ float spow_lds[POWF ? 4 : 1][POWF ? SB : 1];
     __shared__ float4 fused_rad[FUSE ? SB : 1];
     __shared__ int cmp_count[SB / 64], cmp_base[SB / 64];
     work_counts wc;
@@ -757,6 +762,42 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 vec3f c = {0.0f, 0.0f, 0.0f};
                 // raytrace.cpp:147 (per light) and :196 (mirror): the same value each time
                 const vec3f v = normalize(ro - p);
+#if YRT_SHADE_POW_FIRST
+                if constexpr (OCC4) {
+                    // the specular powers first, each in a loop iteration of its own, with
+                    // only what they need live: the f64 exp2/log2 path (rare: most calls
+                    // take spec_pow's exact shortcuts) no longer adds its ~40 VGPRs to the
+                    // full shading state, and the kernel fits 8 waves per SIMD. The inputs
+                    // are the same float operations as in the loop below, so the values
+                    // are the same.
+                    for (int li = 0; li < S.nlights; li++) {
+                        float sp = 1.0f;
+                        if (((occ_bits >> li) & 1u) == 0u) {
+                            float4 lrec[6];
+                            ld_scalar<6>(S.lights + 6 * li, lrec);
+                            const frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
+                            const vec3f lp0 = xyz(lrec[4]), ke = xyz(lrec[5]);
+                            const vec3f tp = transform_point(lf, lp0 - p);
+                            const vec3f l = normalize(tp);
+                            const float r = length(tp);
+                            const vec3f h = normalize(v + l);
+                            vec3f ks = ks0;
+                            if (ks_txt >= 0) ks = ks * tks;
+                            const vec3f ls = ks * (ke / (r * r));
+                            float x;
+                            if (kind == kind_lines) {
+                                float prodnh = dot(nrm, h);
+                                if (prodnh < 0.0f) prodnh *= -1;
+                                x = __builtin_sqrtf(1.0f - prodnh);
+                            } else {
+                                x = smax(0.0f, dot(nrm, h));
+                            }
+                            sp = spec_pow(x, ns, ls);
+                        }
+                        spow_lds[li][threadIdx.x] = sp;
+                    }
+                }
+#endif
                 for (int li = 0; li < S.nlights; li++) {
                     if (OCC4 ? ((occ_bits >> li) & 1u) != 0u : B.occl[(size_t)li * B.capacity + idx] != 0) continue;
                     const f4* lr = S.lights + 6 * li;
@@ -788,10 +829,10 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                         float sinnl = __builtin_sqrtf(1.0f - prodnl);
                         float sinnh = __builtin_sqrtf(1.0f - prodnh);
                         ld = ld * sinnl;
-                        ls = ls * spec_pow(sinnh, ns, ls);
+                        ls = ls * (POWF ? spow_lds[li][threadIdx.x] : spec_pow(sinnh, ns, ls));
                     } else {
                         ld = ld * smax(0.0f, dot(nrm, l));
-                        ls = ls * spec_pow(smax(0.0f, dot(nrm, h)), ns, ls);
+                        ls = ls * (POWF ? spow_lds[li][threadIdx.x] : spec_pow(smax(0.0f, dot(nrm, h)), ns, ls));
                     }
                     c = c + (ld + ls);
                 }
