@@ -318,6 +318,9 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
 #ifndef YRT_PRIMARY_PERSIST
 #define YRT_PRIMARY_PERSIST 0  // A/B at c4: primary +9 % (runs of 256 or 64 blocks alike)
 #endif
+#ifndef YRT_PRIMARY_STRIDE
+#define YRT_PRIMARY_STRIDE 1  // YRT_PRIMARY_PERSIST: a batch's positions one row of waves apart
+#endif
 constexpr int PP_BLOCK = packet_block;  // packet_first parks 1/d per thread in LDS: <= packet_block threads
 template <bool COUNT, bool PACKET, typename SE>
 __global__ __launch_bounds__(PP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(dev_scene_view S, dev_render_args A,
@@ -340,6 +343,27 @@ __global__ __launch_bounds__(PP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(d
     unsigned qv = issue(), qb = 0, qleft = 0;
     unsigned nvalid = 0;  // wave-uniform
     work_counts wc;
+    auto block_of = [&](unsigned q) {
+        return q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
+    };
+#if YRT_PRIMARY_STRIDE
+    // batch k = the G positions (k / W) * W*G + k % W + j*W, j < G (W = the XCD's waves):
+    // waves move through the positions in rows of W together, so the XCD's active window
+    // stays ~W positions wide instead of W*G (each wave's G items come W apart)
+    const unsigned W = gridDim.x / 8u * (PP_BLOCK / 64u);
+    unsigned qk = 0;
+    for (;;) {
+        if (qleft == 0) {
+            qk = (unsigned)__builtin_amdgcn_readfirstlane((int)qv);
+            qleft = G;
+            qv = issue();
+            if (block_of((qk / W) * (W * G) + qk % W) >= n) break;  // positions grow with the batch
+        }
+        const unsigned q = (qk / W) * (W * G) + qk % W + (G - qleft) * W;
+        qleft--;
+        const unsigned b = block_of(q);
+        if (b >= n) continue;
+#else
     for (;;) {
         if (qleft == 0) {
             qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
@@ -348,8 +372,9 @@ __global__ __launch_bounds__(PP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(d
         }
         const unsigned q = qb++;
         qleft--;
-        const unsigned b = q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
+        const unsigned b = block_of(q);
         if (b >= n) break;
+#endif
         const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, (int)(b * 64u + lane), wc);
         nvalid += (unsigned)__popcll(ballot(valid));
     }
