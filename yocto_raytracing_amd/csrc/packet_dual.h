@@ -128,7 +128,7 @@ __device__ __forceinline__ unsigned long long dual_leaf_hits(const dev_scene_vie
             ld_records<3>(S.sprims + 3 * i, pv);
             float t, w1, w2;
             const bool h = tri_hit_nb<YRT_TRI_RCP>(R.co, R.cd, tmin, R.tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t,
-                                                   w1, w2, in);
+                                                   w1, w2, in, ballot(in));
             leaf_hit |= (h && in) ? 1 : 0;
         }
     } else {

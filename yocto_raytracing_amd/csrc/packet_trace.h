@@ -219,6 +219,9 @@ __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, fl
 #ifndef YRT_TRI_RCP_FIRST
 #define YRT_TRI_RCP_FIRST 1  // the same in the closest-hit walk (A/B: primary -0.9 % with the early exits; +0.6 % before them)
 #endif
+#ifndef YRT_TRI_SKIPSEL
+#define YRT_TRI_SKIPSEL 1  // closest hit: skip a triangle's hit-record selects when no lane hits it
+#endif
 #ifndef YRT_TRI_TFIRST
 #define YRT_TRI_TFIRST 0  // closest hit: test the distance before the barycentrics (A/B: primary +3 %)
 #endif
@@ -235,16 +238,22 @@ __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, fl
 // when every such lane has den and 1/den normal (a wave-uniform check), fast_div.h's
 // rcp_nr gives the same bits in three instructions instead of ten. The closest-hit walk
 // does not gain from it (+0.6 %), the any-hit walk does.
+#ifndef YRT_TRI_MASKS
+#define YRT_TRI_MASKS 1  // wave-level exits from one ballot per compare, ANDed on the scalar unit
+#endif
+// `inm`: the same lanes as a wave mask. A ballot of an AND of compares is materialised in a
+// VGPR and compared back (v_cndmask + v_cmp per exit); a ballot of each compare is the
+// compare's own SGPR result, and the ANDs go to the scalar unit.
 template <bool RCP = false, bool TFIRST = false>
 __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float tmax, vec3f v0, vec3f e1, vec3f e2,
-                                           float& t, float& w1, float& w2, bool in) {
+                                           float& t, float& w1, float& w2, bool in, unsigned long long inm) {
     vec3f r = cross(d, e2);
     float den = dot(r, e1);
 #ifdef YRT_EXP_FASTTRI  // timing diagnostic only: approximate reciprocal (results differ)
     float inv_den = __builtin_amdgcn_rcpf(den);
 #else
     float inv_den;
-    if (!RCP || ballot(in && !rcp_nr_ok(den)))
+    if (!RCP || (YRT_TRI_MASKS ? (ballot(!rcp_nr_ok(den)) & inm) != 0 : ballot(in && !rcp_nr_ok(den)) != 0))
         inv_den = 1.0f / den;
     else
         inv_den = rcp_nr(den);
@@ -264,10 +273,12 @@ __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float t
         return (den != 0) & !(w1 < 0 || w1 > 1) & !(w2 < 0.0f || w1 + w2 > 1.0f) & !(t < tmin || t > tmax);
     }
     w1 = dot(r, c) * inv_den;
+    // !(w1 < 0 || w1 > 1) == !(w1 < 0) && !(w1 > 1): a NaN passes both, as in the reference
+    const unsigned long long m1 = YRT_TRI_MASKS ? inm & ballot(den != 0) & ballot(!(w1 < 0)) & ballot(!(w1 > 1)) : 0ull;
 #if YRT_TRI_EARLY
     // no lane that counts passes the first barycentric test: the rest of the test (half of
     // it) cannot make any of them hit
-    if (!ballot(in && (den != 0) && !(w1 < 0 || w1 > 1))) {
+    if (YRT_TRI_MASKS ? m1 == 0 : !ballot(in && (den != 0) && !(w1 < 0 || w1 > 1))) {
         t = w2 = 0.0f;
         return false;
     }
@@ -275,7 +286,8 @@ __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float t
     vec3f s = cross(c, e1);
     w2 = dot(s, d) * inv_den;
 #if YRT_TRI_EARLY2
-    if (!ballot(in && (den != 0) && !(w1 < 0 || w1 > 1) && !(w2 < 0.0f || w1 + w2 > 1.0f))) {
+    if (YRT_TRI_MASKS ? (m1 & ballot(!(w2 < 0.0f)) & ballot(!(w1 + w2 > 1.0f))) == 0
+                      : !ballot(in && (den != 0) && !(w1 < 0 || w1 > 1) && !(w2 < 0.0f || w1 + w2 > 1.0f))) {
         t = 0.0f;
         return false;
     }
@@ -387,7 +399,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     float t, w1, w2;
                     bool h;
                     if (kind == kind_triangles) {
-                        h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2, in);
+                        h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2, in, ballot(in));
                     } else {
                         // lines: ew = {1-s, s, 0, 0}; points: {1, 0, 0, 0} -- both are
                         // {1-w1-w2, w1, w2, 0} with w1 = ew.y, w2 = ew.z
@@ -848,14 +860,17 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                         float t, w1, w2;
                         const bool h =
                             tri_hit_nb<YRT_TRI_RCP_FIRST, YRT_TRI_TFIRST>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]),
-                                                                          xyz(pv[2]), t, w1, w2, in) &&
+                                                                          xyz(pv[2]), t, w1, w2, in, lmask) &&
                             in;
-                        tmax = h ? t : tmax;
-                        hslot = h ? cur_slot : hslot;
-                        hei = h ? ibits(pv[0].w) : hei;
-                        hw1 = h ? w1 : hw1;
-                        hw2 = h ? w2 : hw2;
-                        leaf_hit |= h ? 1 : 0;
+                        // most triangles hit no lane: their record-keeping selects are skipped
+                        if (!YRT_TRI_SKIPSEL || ballot(h)) {
+                            tmax = h ? t : tmax;
+                            hslot = h ? cur_slot : hslot;
+                            hei = h ? ibits(pv[0].w) : hei;
+                            hw1 = h ? w1 : hw1;
+                            hw2 = h ? w2 : hw2;
+                            leaf_hit |= h ? 1 : 0;
+                        }
                     }
                 } else {
                     for (int i = lstart; i < lstart + lcount; i++) {
@@ -1375,7 +1390,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                         ld_records<3>(S.sprims + 3 * i, pv);
                         float t, w1, w2;
                         const bool h =
-                            tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, inl);
+                            tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, inl,
+                                                    mask);
                         leaf_hit |= (h && inl) ? 1 : 0;
                         // every lane of the leaf occluded: the leaf's other triangles cannot
                         // change the answer
