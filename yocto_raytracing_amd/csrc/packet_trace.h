@@ -172,10 +172,17 @@ __device__ __forceinline__ void ld_records(const f4* p, float4 (&out)[N]) {
 // (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
 template <int N>
 __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
-    static_assert(N == 4 || N == 6 || N == 8, "record count");
+    static_assert(N == 3 || N == 4 || N == 6 || N == 8, "record count");
     const f4* base = sgpr_ptr(base_);
     const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
-    if constexpr (N == 4) {
+    if constexpr (N == 3) {
+        sgpr8 a;
+        sgpr4 b;
+        asm volatile("s_load_dwordx8 %0, %2, %3\n s_load_dwordx4 %1, %2, %3 offset:0x20\n s_waitcnt lgkmcnt(0)"
+                     : "=&s"(a), "=&s"(b)
+                     : "s"(base), "s"(off));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(b, 0);
+    } else if constexpr (N == 4) {
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
@@ -204,7 +211,7 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
 template <int N>
 __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, float4 (&out)[N]) {
 #if YRT_SCALAR_LOADS && YRT_SOFF
-    if constexpr (N == 4 || N == 6 || N == 8) {
+    if constexpr (N == 3 || N == 4 || N == 6 || N == 8) {
         ld_scalar_at<N>(base, index, out);
         return;
     }
@@ -854,7 +861,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 if (kind == kind_triangles) {
                     for (int i = lstart; i < lstart + lcount; i++) {
                         float4 pv[3];
-                        ld_records<3>(S.sprims + 3 * i, pv);
+                        ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
                         if (COUNT && in) wc.prim++;
                         if (COUNT && (me & 1)) wc.wprim++;
                         float t, w1, w2;
@@ -875,7 +882,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 } else {
                     for (int i = lstart; i < lstart + lcount; i++) {
                         float4 pv[3];
-                        ld_records<3>(S.sprims + 3 * i, pv);
+                        ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
                         if (COUNT && in) wc.prim++;
                         if (COUNT && (me & 1)) wc.wprim++;
                         // lines: ew = {1-s, s, 0, 0}; points: {1, 0, 0, 0} -- both are
@@ -1387,7 +1394,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 if (kind == kind_triangles) {
                     for (int i = first; i < first + count; i++) {
                         float4 pv[3];
-                        ld_records<3>(S.sprims + 3 * i, pv);
+                        ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
                         float t, w1, w2;
                         const bool h =
                             tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, inl,
@@ -1400,7 +1407,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 } else {
                     for (int i = first; i < first + count; i++) {
                         float4 pv[3];
-                        ld_records<3>(S.sprims + 3 * i, pv);
+                        ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
                         float t;
                         vec4f ew;
                         const ray3 lr = {co, cd, tmin, tmax};
