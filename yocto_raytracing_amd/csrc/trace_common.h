@@ -364,6 +364,15 @@ __device__ __forceinline__ bool occluded(const dev_scene_view& S, const ray3& wr
 #ifndef YRT_POW_SHORTCUT
 #define YRT_POW_SHORTCUT 1  // the exact shortcuts of spec_pow / powf_cr below
 #endif
+#ifndef YRT_POW_CALL
+#define YRT_POW_CALL 1  // the f64 power path as a real call (its registers stay out of the callers' budget)
+#endif
+// the f64 path of powf_cr. Called, not inlined: the f64 log2/exp2 need ~40 VGPRs, which
+// inlined would count against the whole shading kernel's budget; as a call, the caller
+// spills what it has live around it, and only on the (rare) path that needs it.
+__device__ __attribute__((noinline)) float pow_f64_path(float x, float y) {
+    return (float)exp2((double)y * log2((double)x));
+}
 __device__ __forceinline__ float powf_cr(float x, float y) {
 #if YRT_POW_FULL
     return (float)pow((double)x, (double)y);
@@ -375,6 +384,7 @@ __device__ __forceinline__ float powf_cr(float x, float y) {
     if (YRT_POW_SHORTCUT && y > 0.0f &&
         (x == 0.0f || (x >= 0x1p-126f && x < 1.0f && y * __builtin_amdgcn_logf(x) < -151.0f)))
         return 0.0f;
+    if (YRT_POW_CALL) return pow_f64_path(x, y);
     return (float)exp2((double)y * log2((double)x));
 #endif
 }

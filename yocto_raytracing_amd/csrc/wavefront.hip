@@ -713,7 +713,7 @@ __global__ __launch_bounds__(SD_BLOCK, YRT_SHADOW_DUAL_WAVES) void k_shadow_dual
 #define YRT_SHADE_POW_FIRST 0  // k_shade: the specular powers in a pass of their own (A/B: c4 shade +22 %, c3 -5 %; VGPRs 95 natural)
 #endif
 #ifndef YRT_SHADE_WAVES
-#define YRT_SHADE_WAVES 5  // k_shade register budget (its natural 96 VGPRs; A/B: 6 -> +26 %, 8 -> +140 % from spills)
+#define YRT_SHADE_WAVES 7  // k_shade register budget: 65-73 VGPRs with the f64 pow called (A/B at c4: 5 -> 7 waves -4 %; with the pow inlined it needed 96)
 #endif
 // OCC4 (scenes with at most four lights): the occlusion bytes are loaded together with the
 // surface, one memory round trip instead of one per light inside the light loop.
