@@ -558,7 +558,19 @@ device_scene* device_scene_create(const scene& scn, int device) {
         if (ist.mat < 0 || ist.mat >= (int)scn.materials.size())
             throw std::runtime_error("instance " + ist.name + " has no material");
         const frame3f& f = ist.frame;
-        tinst.push_back({f.x.x, f.x.y, f.x.z, as_float(ist.shp)});
+        // the frame's rotation rows bitwise equal to the identity's: the instance-local
+        // direction is then the same for every such instance (the walks compute it once)
+        auto bits = [](float v) {
+            uint32_t u;
+            memcpy(&u, &v, 4);
+            return u;
+        };
+        const bool ident = bits(f.x.x) == 0x3f800000u && bits(f.x.y) == 0 && bits(f.x.z) == 0 && bits(f.y.x) == 0 &&
+                           bits(f.y.y) == 0x3f800000u && bits(f.y.z) == 0 && bits(f.z.x) == 0 && bits(f.z.y) == 0 &&
+                           bits(f.z.z) == 0x3f800000u;
+        if (ist.shp >= (1 << 30)) throw unsupported_error("scene too large (shapes >= 2^30, unsupported)");
+        // .w: the shape index | identity rotation << 30
+        tinst.push_back({f.x.x, f.x.y, f.x.z, as_float((int)((uint32_t)ist.shp | (ident ? inst_identity_bit : 0u)))});
         // .w: the shape's wide root (record byte offset) | kind << 30 (the any-hit walk's entry)
         const uint32_t wr = (uint32_t)wshape_root[ist.shp] * (uint32_t)wide_record_bytes;
         tinst.push_back({f.y.x, f.y.y, f.y.z, as_float((int)(wr | ((uint32_t)shapes[ist.shp].y << 30)))});

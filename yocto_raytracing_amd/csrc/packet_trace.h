@@ -677,6 +677,9 @@ constexpr int packet_block = 256;  // >= threads per block of every kernel that 
 #ifndef YRT_FIRST_HOIST
 #define YRT_FIRST_HOIST 1  // closest-hit descent: the record base made wave-uniform once per descent
 #endif
+#ifndef YRT_IDENT_INST
+#define YRT_IDENT_INST 1  // instances with an identity rotation share one instance-local direction per walk
+#endif
 #ifndef YRT_FIRST_OCTANT
 #define YRT_FIRST_OCTANT 1  // closest hit: octant-specialised slab tests (see box_oct)
 #endif
@@ -818,6 +821,13 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     const f4* pbase = S.tpair;
     const int woct = YRT_FIRST_OCTANT ? wave_octant(ci, live) : 8;
     int oct = woct;
+#if YRT_IDENT_INST
+    // the instance-local direction of the instances with an identity rotation, once per
+    // walk (packet_occluded_wide2 does the same)
+    vec3f icd, ici;
+    enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
+    const int ioct = YRT_FIRST_OCTANT ? wave_octant(ici, live) : 8;
+#endif
     for (;;) {
         // ---- descent: one spine record per step, until a leaf or no passing lane ----
         DBG_CHECK(node >= 0 && (node % spine_record_bytes) == 0 && sp >= 0 && sp < 63 &&
@@ -917,7 +927,13 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-                    enter_direction(f, wd, live & ~done, cd, ci);
+#if YRT_IDENT_INST
+                    const bool ident = (uniform(ibits(fr[0].w)) & (int)inst_identity_bit) != 0;
+                    if (ident)
+                        cd = icd, ci = ici;
+                    else
+#endif
+                        enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[3].w));
                     pbase = S.spair + spine_record_f4 * (rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
@@ -925,7 +941,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     mask = inst_mask & ~done;
                     if (COUNT && (mask & me)) wc.inst++;
                     node = 0;  // the shape root, tested like any popped node
+#if YRT_IDENT_INST
+                    if (YRT_FIRST_OCTANT) oct = ident ? ioct : wave_octant(ci, live & ~done);
+#else
                     if (YRT_FIRST_OCTANT) oct = wave_octant(ci, live & ~done);
+#endif
                     if (mask) break;
                     continue;
                 }
@@ -1346,6 +1366,14 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     // the octant of the current level's rays when the whole wave shares it (8: mixed)
     const int woct = YRT_WIDE_OCTANT ? wave_octant(wi, live) : 8;
     int oct = woct;
+#if YRT_IDENT_INST
+    // the instance-local direction of every instance whose rotation is the identity:
+    // enter_direction on the identity frame is what entering any of them computes, bit for
+    // bit (the same dot products, normalisation and reciprocals), so it is done once here
+    vec3f icd, ici;
+    enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
+    const int ioct = YRT_WIDE_OCTANT ? wave_octant(ici, live) : 8;
+#endif
     unsigned nsteps0 = 0, nsteps1 = 0;
 #ifdef YRT_WIDE_STATS
     unsigned ws[16] = {1, 0, 0, 0, 0, 0, 0, 0};
@@ -1433,7 +1461,13 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     ld_records_at<NR>(YRT_WIDE_ROOTBOX ? S.winst : S.tinst, (unsigned)(NR * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-                    enter_direction(f, wd, live & ~done, cd, ci);
+#if YRT_IDENT_INST
+                    const bool ident = (uniform(ibits(fr[0].w)) & (int)inst_identity_bit) != 0;
+                    if (ident)
+                        cd = icd, ci = ici;
+                    else
+#endif
+                        enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
@@ -1448,7 +1482,11 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                                                 fr[5].z, tn));
                     }
                     WSTAT(3, 1u);
+#if YRT_IDENT_INST
+                    if (YRT_WIDE_OCTANT) oct = ident ? ioct : wave_octant(ci, live & ~done);
+#else
                     if (YRT_WIDE_OCTANT) oct = wave_octant(ci, live & ~done);
+#endif
                     if (mask) break;
                     continue;
                 }

@@ -171,7 +171,7 @@ __device__ __forceinline__ bool traverse(const dev_scene_view& S, ray3 wray, hit
                 ld = transform_direction_inverse(f, wray.d);
                 linvd = {1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z};
                 ltmax = wray.tmax;
-                int4 sh = ld4(S.shapes + ibits(fx.w));
+                int4 sh = ld4(S.shapes + (ibits(fx.w) & (int)inst_shape_mask));
                 root = sh.x;
                 kind = sh.y;
                 cur_slot = k;
@@ -326,7 +326,7 @@ __device__ __forceinline__ bool occluded(const dev_scene_view& S, const ray3& wr
                     co = transform_point_inverse(f, wray.o);
                     ld = transform_direction_inverse(f, wray.d);
                     ci = {1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z};
-                    int4 sh = ld4(S.shapes + ibits(fx.w));
+                    int4 sh = ld4(S.shapes + (ibits(fx.w) & (int)inst_shape_mask));
                     root = sh.x;
                     kind = sh.y;
                     lo = ld4(S.snodes + 2 * root);
@@ -442,7 +442,7 @@ __device__ __forceinline__ surface eval_surface(const dev_scene_view& S, int slo
     const f4* ti = S.tinst + 4 * slot;
     float4 fx = ld4(ti), fy = ld4(ti + 1), fz = ld4(ti + 2), fo = ld4(ti + 3);
     frame3f f = {xyz(fx), xyz(fy), xyz(fz), xyz(fo)};
-    int4 sh = ld4(S.shapes + ibits(fx.w));
+    int4 sh = ld4(S.shapes + (ibits(fx.w) & (int)inst_shape_mask));
     int4 e = ld4(S.elems + sh.z + ei);
     surface sf;
     sf.mat = ibits(fz.w);

@@ -4,7 +4,7 @@
 // Everything is 16-byte records so each fetch is one global_load_dwordx4:
 //   tnodes  2 x f4 per instance-BVH node  {min.xyz, start} {max.xyz, count|leaf<<31}
 //   tinst   4 x f4 per instance-BVH leaf slot (instances permuted to leaf order)
-//           {frame.x, shape} {frame.y, shape wide root | kind << 30} {frame.z, material}
+//           {frame.x, shape | identity << 30} {frame.y, shape wide root | kind << 30} {frame.z, material}
 //           {frame.o, shape root node | kind << 30}
 //   tinst_id int per instance-BVH leaf slot: the instance's index in the scene
 //   snodes  2 x f4 per shape-BVH node, all shapes concatenated, child/leaf indices absolute
@@ -45,6 +45,9 @@ enum shape_kind : int { kind_triangles = 0, kind_lines = 1, kind_points = 2, kin
 enum mat_flags : int { mat_reflective = 1 };
 
 constexpr uint32_t leaf_bit = 0x80000000u;
+// tinst row 0 .w: set when the instance frame's rotation rows are bitwise the identity's
+constexpr uint32_t inst_identity_bit = 0x40000000u;
+constexpr uint32_t inst_shape_mask = 0x3fffffffu;
 
 // 4-wide any-hit records (device_scene.cpp wide_builder): 128 bytes per wide node --
 // six f4 rows of child bounds {lo.x[4]}, {lo.y[4]}, {lo.z[4]}, {hi.x[4]}, {hi.y[4]},
