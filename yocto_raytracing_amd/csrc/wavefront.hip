@@ -712,6 +712,9 @@ __global__ __launch_bounds__(SD_BLOCK, YRT_SHADOW_DUAL_WAVES) void k_shadow_dual
 #ifndef YRT_SHADE_POW_FIRST
 #define YRT_SHADE_POW_FIRST 0  // k_shade: the specular powers in a pass of their own (A/B: c4 shade +22 %, c3 -5 %; VGPRs 95 natural)
 #endif
+#ifndef YRT_SHADE_SUM3
+#define YRT_SHADE_SUM3 1  // fused k_shade: the per-pixel sums one lane per colour component
+#endif
 #ifndef YRT_SHADE_WAVES
 #define YRT_SHADE_WAVES 7  // k_shade register budget: 65-73 VGPRs with the f64 pow called (A/B at c4: 5 -> 7 waves -4 %; with the pow inlined it needed 96)
 #endif
@@ -933,6 +936,28 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
         // raytrace.cpp:232-249: s*s samples of a pixel summed in jj/ii order, then / s*s
         __syncthreads();
         const int ppb = SB / C.spp;
+#if YRT_SHADE_SUM3
+        // one lane per (pixel, colour component): each lane's sum is the same ordered chain
+        // of adds as the float4 loop below, with a third of the dependent adds per lane
+        for (int t = (int)threadIdx.x; t < 3 * ppb; t += SB) {
+            const int px = t / 3, comp = t - 3 * px;
+            const int pl = (int)(blockIdx.x * SB / C.spp) + px;
+            int lx, ly, i, j;
+            const bool valid = pl < C.npix && pixel_of(A, C.tiles_x, C.pix0 + pl, lx, ly, i, j);
+            if (pl < C.npix && lx < A.tile_w && ly < A.tile_h) {
+                float v = 0.0f;
+                if (valid) {
+                    const float* r = reinterpret_cast<const float*>(fused_rad + px * C.spp) + comp;
+                    float acc = 0.0f;
+                    for (int q = 0; q < C.spp; q++) acc = acc + r[4 * q];
+                    v = acc / float(C.spp);
+                }
+                float* o = reinterpret_cast<float*>(out + (size_t)ly * A.out_stride + lx);
+                o[comp] = v;
+                if (comp == 0) o[3] = valid ? 1.0f : 0.0f;
+            }
+        }
+#else
         if ((int)threadIdx.x < ppb) {
             const int pl = (int)(blockIdx.x * SB / C.spp) + threadIdx.x;
             int lx, ly, i, j;
@@ -952,6 +977,7 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 out[(size_t)ly * A.out_stride + lx] = o;
             }
         }
+#endif
     }
     flush<false>(counters, cnt_depth_truncated, truncated);
     if (COUNT) flush_work(counters, wc);
