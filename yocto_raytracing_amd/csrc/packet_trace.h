@@ -1001,6 +1001,38 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
 
+#ifndef YRT_WIDE_R7
+#define YRT_WIDE_R7 0  // 1: a wide step loads the record's last row (its slot count) too
+#endif
+
+// A wide record through the scalar cache. Without YRT_WIDE_R7 only its first 112 bytes
+// (bounds and child words: x16 + x8 + x4, 28 SGPRs instead of 32) -- the slot count in the
+// last row is implied by the child words, an empty slot's word being wide_leaf exactly (a
+// leaf of no primitives: skipping one changes nothing).
+__device__ __forceinline__ void ld_wide_record(const f4* wbase, uint32_t off, float4 (&r)[8]) {
+#if YRT_WIDE_R7
+    sgpr16 a, b;
+    asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b)
+                 : "s"(wbase), "s"(uniform((int)off)));
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
+#else
+    sgpr16 a;
+    sgpr8 b;
+    sgpr4 c;
+    asm volatile(
+        "s_load_dwordx16 %0, %3, %4\n s_load_dwordx8 %1, %3, %4 offset:0x40\n s_load_dwordx4 %2, %3, %4 offset:0x60\n"
+        " s_waitcnt lgkmcnt(0)"
+        : "=&s"(a), "=&s"(b), "=&s"(c)
+        : "s"(wbase), "s"(uniform((int)off)));
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] = rec_of(a, k);
+    r[4] = rec_of(b, 0), r[5] = rec_of(b, 1), r[6] = rec_of(c, 0);
+    r[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#endif
+}
+
 // the slab tests of a wide step on the record r: m[k] = the lanes of `mask` that pass
 // slot k's box (0 for a slot the node does not have), w[k] = slot k's child word
 template <int OCT>
@@ -1011,7 +1043,8 @@ __device__ __forceinline__ void wide_tests(const float4 (&r)[8], vec3f co, vec3f
                 hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
     w[0] = (uint32_t)uniform(ibits(r[6].x)), w[1] = (uint32_t)uniform(ibits(r[6].y));
     w[2] = (uint32_t)uniform(ibits(r[6].z)), w[3] = (uint32_t)uniform(ibits(r[6].w));
-    const int nslots = uniform(ibits(r[7].x));
+    // whether slot k (k >= 2) exists: the record's slot count, or its child word
+    auto has = [&](int k) { return YRT_WIDE_R7 ? k < uniform(ibits(r[7].x)) : w[k] != wide_leaf; };
     if constexpr (YRT_PK_BOX && OCT < 8) {
         // slots 0 and 1 always (a leaf root's empty slot 1 fails its test), 2 and 3
         // when the node has a third slot; a missing fourth is masked out
@@ -1021,17 +1054,17 @@ __device__ __forceinline__ void wide_tests(const float4 (&r)[8], vec3f co, vec3f
         m[0] = ballot(p0) & mask;
         m[1] = ballot(p1) & mask;
         m[2] = m[3] = 0;
-        if (nslots > 2) {
+        if (has(2)) {
             bool p2, p3;
             box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[2], lx[3]}, f2v{ly[2], ly[3]}, f2v{lz[2], lz[3]},
                               f2v{hx[2], hx[3]}, f2v{hy[2], hy[3]}, f2v{hz[2], hz[3]}, p2, p3);
             m[2] = ballot(p2) & mask;
-            m[3] = nslots > 3 ? ballot(p3) & mask : 0ull;
+            m[3] = has(3) ? ballot(p3) & mask : 0ull;
         }
     } else {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            if (!YRT_WIDE_SKIP || k < 2 || k < nslots)  // every wide node has >= 2 slots but a leaf root's 1
+            if (!YRT_WIDE_SKIP || k < 2 || has(k))  // every wide node has >= 2 slots but a leaf root's 1
                 m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
             else
                 m[k] = 0;
@@ -1263,12 +1296,7 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, const floa
 #pragma unroll
             for (int k = 0; k < 8; k++) r[k] = p[k];
         } else {
-            sgpr16 a, b;
-            asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                         : "=&s"(a), "=&s"(b)
-                         : "s"(wbase), "s"(uniform((int)cur)));
-#pragma unroll
-            for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
+            ld_wide_record(wbase, cur, r);
         }
         uint32_t w[4];
         unsigned long long m[4];
@@ -1327,12 +1355,7 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, const floa
             more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         } else {
             float4 r[8];
-            sgpr16 a, b;
-            asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                         : "=&s"(a), "=&s"(b)
-                         : "s"(wbase), "s"(uniform((int)cur)));
-#pragma unroll
-            for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
+            ld_wide_record(wbase, cur, r);
             more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         }
         if (!more) return;
