@@ -582,13 +582,18 @@ device_scene* device_scene_create(const scene& scn, int device) {
         if (sh.x >= (1 << 30)) throw unsupported_error("scene too large (shape nodes >= 2^30, unsupported)");
         tinst.push_back({f.o.x, f.o.y, f.o.z, as_float((int)((uint32_t)sh.x | ((uint32_t)sh.y << 30)))});
         // any-hit copy with the shape's root box (an empty shape: a box no finite ray passes)
-        winst.insert(winst.end(), tinst.end() - 4, tinst.end());
         const shape& sp = scn.shapes[ist.shp];
-        if (sp.bvh.nodes.empty()) {
-            winst.push_back({INFINITY, INFINITY, INFINITY, 0});
-            winst.push_back({-INFINITY, -INFINITY, -INFINITY, 0});
+        bbox3f rb = {{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+        if (!sp.bvh.nodes.empty()) rb = sp.bvh.nodes[0].bbox;
+        if (winst_rows == 5) {
+            const f4* t = &tinst[tinst.size() - 4];
+            winst.push_back(t[0]);
+            winst.push_back(t[1]);
+            winst.push_back({t[2].x, t[2].y, t[2].z, rb.min.x});
+            winst.push_back({t[3].x, t[3].y, t[3].z, rb.min.y});
+            winst.push_back({rb.min.z, rb.max.x, rb.max.y, rb.max.z});
         } else {
-            const bbox3f& rb = sp.bvh.nodes[0].bbox;
+            winst.insert(winst.end(), tinst.end() - 4, tinst.end());
             winst.push_back({rb.min.x, rb.min.y, rb.min.z, 0});
             winst.push_back({rb.max.x, rb.max.y, rb.max.z, 0});
         }

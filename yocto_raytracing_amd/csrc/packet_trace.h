@@ -172,7 +172,7 @@ __device__ __forceinline__ void ld_records(const f4* p, float4 (&out)[N]) {
 // (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
 template <int N>
 __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
-    static_assert(N == 3 || N == 4 || N == 6 || N == 8, "record count");
+    static_assert(N == 3 || N == 4 || N == 5 || N == 6 || N == 8, "record count");
     const f4* base = sgpr_ptr(base_);
     const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
     if constexpr (N == 3) {
@@ -186,6 +186,14 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+    } else if constexpr (N == 5) {
+        sgpr16 a;
+        sgpr4 b;
+        asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx4 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                     : "=&s"(a), "=&s"(b)
+                     : "s"(base), "s"(off));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+        out[4] = rec_of(b, 0);
     } else if constexpr (N == 6) {
         sgpr16 a;
         sgpr8 b;
@@ -211,12 +219,14 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
 template <int N>
 __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, float4 (&out)[N]) {
 #if YRT_SCALAR_LOADS && YRT_SOFF
-    if constexpr (N == 3 || N == 4 || N == 6 || N == 8) {
+    if constexpr (N == 3 || N == 4 || N == 5 || N == 6 || N == 8) {
         ld_scalar_at<N>(base, index, out);
         return;
-    }
+    } else
 #endif
-    ld_records<N>(base + index, out);
+    {
+        ld_records<N>(base + index, out);
+    }
 }
 
 
@@ -1479,8 +1489,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 if (inst_next < inst_end) {
                     const int k = inst_next++;
                     DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_end, sp, base, 0);
-                    float4 fr[YRT_WIDE_ROOTBOX ? 6 : 4];
-                    constexpr int NR = YRT_WIDE_ROOTBOX ? 6 : 4;
+                    constexpr int NR = YRT_WIDE_ROOTBOX ? winst_rows : 4;
+                    float4 fr[NR];
                     ld_records_at<NR>(YRT_WIDE_ROOTBOX ? S.winst : S.tinst, (unsigned)(NR * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
@@ -1501,8 +1511,12 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                         // fails it finds nothing in this instance (every box below is
                         // inside it)
                         float tn;
-                        mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[4].x, fr[4].y, fr[4].z, fr[5].x, fr[5].y,
-                                                fr[5].z, tn));
+                        if constexpr (winst_rows == 5)
+                            mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[2].w, fr[3].w, fr[4].x, fr[4].y, fr[4].z,
+                                                    fr[4].w, tn));
+                        else
+                            mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[4].x, fr[4].y, fr[4].z, fr[NR - 1].x,
+                                                    fr[NR - 1].y, fr[NR - 1].z, tn));
                     }
                     WSTAT(3, 1u);
 #if YRT_IDENT_INST

@@ -49,6 +49,15 @@ constexpr uint32_t leaf_bit = 0x80000000u;
 constexpr uint32_t inst_identity_bit = 0x40000000u;
 constexpr uint32_t inst_shape_mask = 0x3fffffffu;
 
+// winst (the any-hit walk's instance records): YRT_WINST5 packs what that walk reads into
+// five rows -- {frame.x, tinst row 0 .w} {frame.y, wide root | kind} {frame.z, box lo.x}
+// {frame.o, box lo.y} {box lo.z, hi.x, hi.y, hi.z} -- one s_load_dwordx16 + x4 (20 SGPRs)
+// instead of tinst's four rows plus two box rows (x16 + x8, 24 SGPRs)
+#ifndef YRT_WINST5
+#define YRT_WINST5 1
+#endif
+constexpr int winst_rows = YRT_WINST5 ? 5 : 6;
+
 // 4-wide any-hit records (device_scene.cpp wide_builder): 128 bytes per wide node --
 // six f4 rows of child bounds {lo.x[4]}, {lo.y[4]}, {lo.z[4]}, {hi.x[4]}, {hi.y[4]},
 // {hi.z[4]}, one f4 of child words, one f4 {slot count, -, -, -}. A child word is the
