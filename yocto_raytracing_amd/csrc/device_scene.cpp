@@ -649,6 +649,15 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_tinst = ab.add(tinst.data(), tinst.size() * sizeof(f4));
     size_t o_snodes = ab.add(snodes.data(), snodes.size() * sizeof(f4));
     size_t o_sprims = ab.add(sprims.data(), sprims.size() * sizeof(f4));
+    // the any-hit walk's triangles: v0, e1, e2 of every sprims slot as 9 packed floats
+    // (one s_load_dwordx8 + s_load_dword, 9 SGPRs instead of 12; other kinds: zeros)
+    std::vector<float> aprims(9 * (sprims.size() / 3), 0.0f);
+    for (size_t i = 0; i < sprims.size() / 3; i++) {
+        const f4* r = &sprims[3 * i];
+        const float v[9] = {r[0].x, r[0].y, r[0].z, r[1].x, r[1].y, r[1].z, r[2].x, r[2].y, r[2].z};
+        for (int q = 0; q < 9; q++) aprims[9 * i + q] = v[q];
+    }
+    size_t o_aprims = ab.add(aprims.data(), aprims.size() * sizeof(float));
     size_t o_shapes = ab.add(shapes.data(), shapes.size() * sizeof(i4));
     size_t o_elems = ab.add(elems.data(), elems.size() * sizeof(i4));
     size_t o_vpos = ab.add(vpos.data(), vpos.size() * sizeof(f4));
@@ -691,6 +700,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.tinst = (const f4*)(base + o_tinst);
     v.snodes = (const f4*)(base + o_snodes);
     v.sprims = (const f4*)(base + o_sprims);
+    v.aprims = (const float*)(base + o_aprims);
     v.shapes = (const i4*)(base + o_shapes);
     v.elems = (const i4*)(base + o_elems);
     v.vpos = (const f4*)(base + o_vpos);

@@ -1011,6 +1011,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
 #define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
 #endif
 
+#ifndef YRT_APRIMS
+#define YRT_APRIMS 1  // any hit: triangles from the packed 9-float array (aprims)
+#endif
 #ifndef YRT_WIDE_R7
 #define YRT_WIDE_R7 0  // 1: a wide step loads the record's last row (its slot count) too
 #endif
@@ -1454,12 +1457,27 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 WSTAT(5, (unsigned)count);
                 if (kind == kind_triangles) {
                     for (int i = first; i < first + count; i++) {
+                        float t, w1, w2;
+#if YRT_APRIMS
+                        // v0, e1, e2 as 9 packed dwords (yrt_device.h aprims): 9 SGPRs, not 12
+                        const f4* abase = sgpr_ptr(reinterpret_cast<const f4*>(S.aprims));
+                        sgpr8 a;
+                        int b;
+                        asm volatile("s_load_dwordx8 %0, %2, %3\n s_load_dword %1, %2, %3 offset:0x20\n"
+                                     " s_waitcnt lgkmcnt(0)"
+                                     : "=&s"(a), "=&s"(b)
+                                     : "s"(abase), "s"(uniform(i * 36)));
+                        const vec3f tv0 = {__int_as_float(a[0]), __int_as_float(a[1]), __int_as_float(a[2])};
+                        const vec3f te1 = {__int_as_float(a[3]), __int_as_float(a[4]), __int_as_float(a[5])};
+                        const vec3f te2 = {__int_as_float(a[6]), __int_as_float(a[7]), __int_as_float(b)};
+                        const bool h = tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, tv0, te1, te2, t, w1, w2, inl, mask);
+#else
                         float4 pv[3];
                         ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
-                        float t, w1, w2;
                         const bool h =
                             tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, inl,
                                                     mask);
+#endif
                         leaf_hit |= (h && inl) ? 1 : 0;
                         // every lane of the leaf occluded: the leaf's other triangles cannot
                         // change the answer

@@ -24,7 +24,9 @@
 //           instance level and all shapes in one array, absolute indices
 //   winst   6 x f4 per instance-BVH leaf slot for the any-hit walk: tinst's four rows, then
 //           the object-space root box of the instance's shape {lo, -} {hi, -} (the box the
-//           reference tests first on entering it, scene.cpp:386-442)
+//           reference tests first on entering it, scene.cpp:386-442); five rows with
+//           YRT_WINST5 (see winst_rows)
+//   aprims  9 floats per sprims slot: a triangle's v0, e1, e2 packed (the any-hit leaf loads)
 #pragma once
 
 #include <stdint.h>
@@ -99,6 +101,7 @@ struct dev_scene_view {
     const float* srgb;
     const f4* wnodes;
     const f4* winst;
+    const float* aprims;  // 9 floats per sprims slot: a triangle's v0, e1, e2 (any-hit walk)
     const f4* tpair;  // 2*spine_len x f4 per instance-BVH node: its record, then its
                       // child start+1's, that child's start+1's, ... (right spine)
     const f4* spair;  // the same for the shape BVHs (same indexing as snodes)
