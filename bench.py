@@ -227,23 +227,49 @@ def cpu_baseline_all_cores(scene_file: Path, res: int, width: int, spp_axis: int
 
 # ---------------------------------------------------------------- roofline
 
-def issue_roofline(issue_json: Path, key: str, kernel_ms: float, key_n1: str = "", share: float = 1.0):
-    """achieved issue rate of the dominant kernel: its committed per-launch instruction
-    counts / the live launch time. At N > 1 ranks without counters of that exact run, the
-    single-GPU counts of the same frame are scaled by this rank's share of the frame's rays
-    (the walks' instruction counts follow the rays they trace; the result says so)."""
+def frame_digest(frame) -> str:
+    """sha256 of a float32 RGBA frame's bytes in image order (host copy, untimed)"""
+    import hashlib
+
+    return hashlib.sha256(frame.detach().contiguous().cpu().numpy().tobytes()).hexdigest()
+
+
+def load_counters(path: Path, key: str, identity: str):
+    """the committed counter record for `key`, if it was collected from a library with
+    this code identity: (record, None), else (None, why not)"""
     try:
-        table = json.loads(issue_json.read_text())
+        table = json.loads(Path(path).read_text())
     except (OSError, ValueError):
-        table = {}
+        return None, f"no counter file {path}"
     rec = table.get(key)
-    if rec is None and key_n1 and key_n1 in table:
-        rec = dict(table[key_n1])
-        for c in ("SQ_INSTS_SALU", "SQ_INSTS_VALU"):
-            rec[c] = rec[c] * share
-        rec["source"] = f"{rec.get('source')} (n1 counts x this rank's ray share {share:.4f})"
-    if not rec or kernel_ms <= 0:
-        return None
+    if rec is None:
+        return None, f"no committed counters for {key}"
+    if rec.get("code_identity") != identity:
+        return None, (f"committed counters for {key} come from another build (code identity "
+                      f"{str(rec.get('code_identity'))[:12]}, timed library {identity[:12]})")
+    return rec, None
+
+
+def issue_roofline(issue_json: Path, key: str, kernel_ms: float, identity: str, key_n1: str = "",
+                   share: float = 1.0):
+    """achieved issue rate of the dominant kernel: its committed per-launch instruction
+    counts / the live launch time -- only when the counters were collected from a library
+    with the timed library's code identity. At N > 1 ranks without counters of that exact
+    run, the single-GPU counts of the same frame are scaled by this rank's share of the
+    frame's rays (the walks' instruction counts follow the rays they trace; the result
+    says so). Returns (bound, pipes, record) or (None, None, why not)."""
+    rec, why = load_counters(issue_json, key, identity)
+    if rec is None and key_n1:
+        rec1, why1 = load_counters(issue_json, key_n1, identity)
+        if rec1 is not None:
+            rec = dict(rec1)
+            for c in ("SQ_INSTS_SALU", "SQ_INSTS_VALU"):
+                rec[c] = rec[c] * share
+            rec["source"] = f"{rec.get('source')} (n1 counts x this rank's ray share {share:.4f})"
+    if rec is None:
+        return None, None, why
+    if kernel_ms <= 0:
+        return None, None, "no launch time"
     s = kernel_ms / 1e3
     salu = rec["SQ_INSTS_SALU"] / s / 1e9
     valu = rec["SQ_INSTS_VALU"] / s / 1e9
@@ -294,6 +320,8 @@ def main():
             dist.init_process_group(backend)
 
     import yocto_raytracing_amd as yrt
+    from yocto_raytracing_amd import _native as yrt_native
+    from yocto_raytracing_amd.codeid import code_identity
 
     scene_file = ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.yrtscene"
     scn = yrt.load_scene(str(scene_file))
@@ -390,6 +418,11 @@ def main():
     if world > 1:
         dist.barrier()
     e2e_ms = (time.perf_counter() - t1) / e2e_frames * 1e3
+    # rank 0's reassembled float frame (every step renders the same frame): an N-rank
+    # line can be checked bit for bit against the N = 1 line
+    frame_sha256 = None
+    if rank == 0 and not a.profile_rank:
+        frame_sha256 = frame_digest(frames[b])
 
     t = torch.tensor([elapsed, dom_ms, render_ms, e2e_ms], dtype=torch.float64, device=dev)
     rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps], dtype=torch.float64, device=dev)
@@ -405,21 +438,18 @@ def main():
         metric = BASELINE_METRIC if is_c4 else f"Mrays/sec + ms/frame, {a.scene} {W}×{H}×{spp}spp, {world} MI355X"
         key = f"{a.scene}-{W}x{H}-s{a.samples}-n{band_world}-{a.algorithm}-{dom}"
         kernel_ms = dom_ms / dom_launches
-        traffic = None
-        try:
-            tr = json.loads(Path(a.traffic_json).read_text())
-            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+        identity = code_identity(yrt_native.LIB_PATH)
+        tr, _ = load_counters(Path(a.traffic_json), key, identity)
+        traffic = tr.get("hbm_bytes_per_launch") if tr else None
         key_n1 = f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-{dom}"
         share = (st["rays"] * a.steps) / total_rays if total_rays else 1.0  # rank 0's share of the frame
-        issue = issue_roofline(Path(a.issue_json), key, kernel_ms, key_n1, share)
-        if issue:
-            bound, pipes, rec = issue
+        bound, pipes, rec = issue_roofline(Path(a.issue_json), key, kernel_ms, identity, key_n1, share)
+        if bound:
             roof = {"bound": "issue", "pipe": bound, "achieved": pipes[bound]["achieved"],
                     "peak": pipes[bound]["peak"], "unit": "G wave-instructions/s", "frac": pipes[bound]["frac"],
                     "traffic": traffic, "kernel": rec.get("kernel", PHASE_KERNEL.get(dom, dom)), "kernel_ms": kernel_ms,
                     "pipes": pipes, "counters": rec.get("source"),
+                    "code_identity": identity,
                     "hbm": {"bytes_per_launch": traffic,
                             "achieved_GBs": traffic / (kernel_ms / 1e3) / 1e9 if traffic else None,
                             "peak_GBs": HBM_PEAK_GBS,
@@ -429,8 +459,8 @@ def main():
         else:
             roof = {"bound": "issue", "achieved": None, "peak": None, "unit": "G wave-instructions/s",
                     "frac": None, "traffic": traffic, "kernel": PHASE_KERNEL.get(dom, dom),
-                    "kernel_ms": kernel_ms,
-                    "note": f"no committed instruction counters for {key} (tools/gpu_issue_pmc.sh)"}
+                    "kernel_ms": kernel_ms, "code_identity": identity,
+                    "note": f"{rec} (tools/gpu_issue_pmc.sh collects them)"}
         line = {
             "metric": metric,
             "value": total_rays / elapsed / 1e6,
@@ -458,6 +488,7 @@ def main():
                        "camera_Msamples_per_s": total_samples / elapsed / 1e6,
                        "algorithm": a.algorithm},
             "roofline": roof,
+            "frame_sha256": frame_sha256,
         }
         if a.profile_rank:  # a counter-collection run, not a bench result
             line["metric"] = f"profile of rank {a.profile_rank} (bands only, no gather): {metric}"

@@ -1,0 +1,70 @@
+"""Build-only checks of the compile-time knobs that survive in the device code.
+
+The product is built with every knob at its default (yocto_raytracing_amd/build.py).
+The knobs that remain are either tunables with a measured default (register
+budgets, block sizes, XCD run lengths, the persistent-grid threshold) or kept
+variants the ledger refers to (LDS staging of the top 4-wide records, the north
+star's "hot node tiles in LDS") and the two diagnostic builds. None of them is
+compiled by the normal build, so each non-default setting is compiled here for
+gfx950 (device code only) to keep it from rotting. A knob added to the sources
+without an entry below fails test_every_knob_is_listed.
+"""
+import concurrent.futures as cf
+import os
+import re
+import subprocess
+
+import pytest
+
+from helpers import ROOT
+
+CSRC = ROOT / "yocto_raytracing_amd" / "csrc"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# knob -> the non-default defines compiled here
+VARIANTS = {
+    "YRT_SHADOW_LDS_RECORDS": ["-DYRT_SHADOW_LDS_RECORDS=85"],
+    "YRT_DEBUG_BOUNDS": ["-DYRT_DEBUG_BOUNDS"],
+    "YRT_WIDE_STATS": ["-DYRT_WIDE_STATS"],
+    "YRT_TRACE_WAVES": ["-DYRT_TRACE_WAVES=7"],
+    "YRT_SHADOW_WAVES": ["-DYRT_SHADOW_WAVES=6"],
+    "YRT_SHADE_WAVES": ["-DYRT_SHADE_WAVES=5"],
+    "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_GRAB=4",
+                          "-DYRT_SHADOW_LIGHT_MINOR=16", "-DYRT_XCD_CHUNK_PRIMARY=64",
+                          "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0"],
+}
+# knobs covered by another entry's defines
+COVERED = {"YRT_SHADOW_BLOCK", "YRT_SHADOW_GRAB", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
+           "YRT_SHADOW_PERSIST_MIN_ITEMS"}
+
+
+def _knobs_in_sources():
+    found = set()
+    for p in list(CSRC.glob("*.h")) + list(CSRC.glob("*.hip")) + list(CSRC.glob("*.cpp")):
+        found |= set(re.findall(r"#\s*if(?:n?def)?\s+(YRT_[A-Z0-9_]+)", p.read_text()))
+    return found
+
+
+def test_every_knob_is_listed():
+    knobs = _knobs_in_sources()
+    assert knobs, "no knobs found"
+    missing = knobs - set(VARIANTS) - COVERED
+    assert not missing, f"knobs without a build-only variant: {sorted(missing)}"
+    stale = (set(VARIANTS) | COVERED) - knobs
+    assert not stale, f"listed knobs no longer in the sources: {sorted(stale)}"
+
+
+def _compile(defs):
+    cmd = [HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", f"-I{CSRC}", f"-I{ROOT / 'include'}", "-mllvm",
+           "-structurizecfg-skip-uniform-regions=true", "-fno-slp-vectorize", "--offload-arch=gfx950",
+           "--offload-device-only", "-c", str(CSRC / "wavefront.hip"), "-o", os.devnull, *defs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    return defs, r.returncode, r.stderr[-3000:]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_non_default_knobs_compile():
+    with cf.ThreadPoolExecutor(max_workers=min(len(VARIANTS), max(1, (os.cpu_count() or 2) - 1))) as ex:
+        results = list(ex.map(_compile, VARIANTS.values()))
+    failed = [(d, err) for d, rc, err in results if rc != 0]
+    assert not failed, "\n".join(f"{d}:\n{err}" for d, err in failed)

@@ -1,7 +1,7 @@
 """Build variants of libyrt.so that differ only in compile-time defines of the
 kernels, for in-process A/B timing (tools/ab_variants.py).
 
-    python tools/build_variants.py scalar:-DYRT_SCALAR_LOADS=1 vec:-DYRT_SCALAR_LOADS=0
+    python tools/build_variants.py w7:-DYRT_TRACE_WAVES=7 lds85:-DYRT_SHADOW_LDS_RECORDS=85
 
 writes yocto_raytracing_amd/variants/libyrt_<name>.so (git-ignored, travels to the GPU box).
 """

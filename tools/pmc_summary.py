@@ -13,6 +13,9 @@ Per timed kernel (COUNT=false, first template argument) and per launch:
   SALU busy = SQ_INSTS_SALU / (256 CUs x cycles) (one scalar unit per CU, one issue per
   clock); VALU busy = SQ_INSTS_VALU / (256 x 4 SIMDs x cycles / 2) (a wave64 VALU
   instruction takes two clocks on a SIMD-32); scalar-cache hit rate.
+Every entry is stamped with the code identity (yocto_raytracing_amd/codeid.py) of the
+library the counters were collected from (--lib): bench.py pairs committed counters
+only with a timed library of the same identity.
 Entries are merged into the existing files (same key = replaced).
 """
 from __future__ import annotations
@@ -21,8 +24,18 @@ import argparse
 import collections
 import csv
 import json
+import importlib.util
 import re
 from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def code_identity(lib: Path) -> str:
+    spec = importlib.util.spec_from_file_location("yrt_codeid", ROOT / "yocto_raytracing_amd" / "codeid.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.code_identity(lib)
 
 PHASE_OF = {"k_primary": "primary", "k_primary_persist": "primary", "k_shadow": "shadow",
             "k_shadow_persist": "shadow", "k_shade": "shade", "k_bounce": "bounce",
@@ -68,7 +81,10 @@ def main():
     ap.add_argument("--source", default="", help="where the CSVs are committed")
     ap.add_argument("--traffic", default="profiles/pmc_traffic.json")
     ap.add_argument("--issue", default="profiles/issue_counters.json")
+    ap.add_argument("--lib", default=str(ROOT / "yocto_raytracing_amd" / "libyrt.so"),
+                    help="the library the counters were collected from (its code identity is stamped)")
     a = ap.parse_args()
+    ident = code_identity(Path(a.lib))
     data = per_launch(a.csv)
     traffic = json.loads(Path(a.traffic).read_text()) if Path(a.traffic).exists() else {}
     issue = json.loads(Path(a.issue).read_text()) if Path(a.issue).exists() else {}
@@ -80,10 +96,11 @@ def main():
             f, w = c["FETCH_SIZE"], c["WRITE_SIZE"]
             traffic[key] = {"kernel": k, "fetch_size_kb": f, "write_size_kb": w,
                             "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024, "source": a.source,
+                            "code_identity": ident,
                             "note": "2*FETCH_SIZE (gfx950 half-count on 16B/lane streams) + WRITE_SIZE, KB->B"}
         rec = {n: v for n, v in c.items() if n.startswith(("SQ_", "SQC_", "GRBM_"))}
         if "SQ_INSTS_SALU" in rec and "SQ_INSTS_VALU" in rec:
-            rec = {"kernel": k, "source": a.source, **rec}
+            rec = {"kernel": k, "source": a.source, "code_identity": ident, **rec}
             cyc = rec.get("GRBM_GUI_ACTIVE", 0) / 8
             if cyc:
                 rec["cycles"] = cyc

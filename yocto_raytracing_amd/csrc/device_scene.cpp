@@ -192,25 +192,8 @@ struct wide_builder {
             const vec3f d = b.max - b.min;
             return d.x * d.y + d.y * d.z + d.z * d.x;
         };
-#ifndef YRT_WIDE_GREEDY
-#define YRT_WIDE_GREEDY 0  // largest-area-first collapse (A/B: instance-level steps 7.06 -> 6.76 per walk, shadow time unchanged)
-#endif
         if (n.isleaf) {
             slots.push_back(x);
-        } else if (YRT_WIDE_GREEDY) {
-            // x's two children, then while there is room the inner slot with the largest
-            // surface area is replaced by its two children (the slot most rays reach is
-            // opened first): up to four slots whichever levels they come from
-            slots = {(int)n.start + 1, (int)n.start};
-            while (slots.size() < 4) {
-                int best = -1;
-                for (int k = 0; k < (int)slots.size(); k++)
-                    if (!t.nodes[slots[k]].isleaf && (best < 0 || area(slots[k]) > area(slots[best]))) best = k;
-                if (best < 0) break;
-                const bvh_node& cn = t.nodes[slots[best]];
-                slots[best] = (int)cn.start + 1;
-                slots.insert(slots.begin() + best + 1, (int)cn.start);
-            }
         } else {
             for (int c : {(int)n.start + 1, (int)n.start}) {  // the reference visits start+1 first
                 const bvh_node& cn = t.nodes[c];
@@ -225,23 +208,7 @@ struct wide_builder {
         // The any-hit walk enters the first passing slot and pops the others in slot
         // order; the order does not change any answer. Smallest surface area first
         // (A/B at c4: shadow -2.7 %; largest first +1.7 %).
-#ifndef YRT_WIDE_SORT
-#define YRT_WIDE_SORT -1
-#endif
-        if (YRT_WIDE_SORT == 3)  // lowest first (experiment: up-going shadow rays)
-            std::stable_sort(slots.begin(), slots.end(),
-                             [&](int a, int b) { return t.nodes[a].bbox.min.y < t.nodes[b].bbox.min.y; });
-        else if (YRT_WIDE_SORT == 4)  // highest first
-            std::stable_sort(slots.begin(), slots.end(),
-                             [&](int a, int b) { return t.nodes[a].bbox.max.y > t.nodes[b].bbox.max.y; });
-        else if (YRT_WIDE_SORT == 2)  // leaves first, then smallest
-            std::stable_sort(slots.begin(), slots.end(), [&](int a, int b) {
-                const bool la = t.nodes[a].isleaf, lb = t.nodes[b].isleaf;
-                return la != lb ? la : area(a) < area(b);
-            });
-        else if (YRT_WIDE_SORT != 0)
-            std::stable_sort(slots.begin(), slots.end(),
-                             [&](int a, int b) { return YRT_WIDE_SORT > 0 ? area(a) > area(b) : area(a) < area(b); });
+        std::stable_sort(slots.begin(), slots.end(), [&](int a, int b) { return area(a) < area(b); });
         return slots;
     }
 
@@ -438,21 +405,16 @@ device_scene* device_scene_create(const scene& scn, int device) {
     }
 
     // ---- 4-wide collapse for the any-hit walk: instance level first, then shapes ----
-    // over the reference trees, or (YRT_WIDE_SAH) over SAH trees of their leaves
-#ifndef YRT_WIDE_SAH
-#define YRT_WIDE_SAH 1
-#endif
+    // over binned-SAH trees of the reference trees' leaves
     auto any_tree = [](const bvh_tree& t) {
-        if (!YRT_WIDE_SAH || t.nodes.empty()) return t;
+        if (t.nodes.empty()) return t;
         sah_builder sb(t);
         return sb.out;
     };
     std::vector<f4> wnodes;
     wide_builder wb{wnodes};
-#ifndef YRT_WIDE_TOP_BFS
-#define YRT_WIDE_TOP_BFS 1  // instance-level wide records in breadth-first order (top levels first)
-#endif
-    const int wtop_root = YRT_WIDE_TOP_BFS ? wb.emit_bfs(any_tree(scn.bvh), 0, 0) : wb.emit(any_tree(scn.bvh), 0, 0, 1);
+    // instance-level wide records breadth first (the top levels lead: what LDS staging reads)
+    const int wtop_root = wb.emit_bfs(any_tree(scn.bvh), 0, 0);
     const int wtop_depth = wb.max_depth;
     const int wtop_records = (int)wnodes.size() / 8;
     std::vector<int> wshape_root(scn.shapes.size());
@@ -520,29 +482,6 @@ device_scene* device_scene_create(const scene& scn, int device) {
                 else
                     y = base + start + 1;
             }
-            if (YRT_FIRST_FILTER) {
-                // the filter boxes: L = X's child start, RL = R's child start (R = X's
-                // child start+1); zero where the parent is a leaf (never read then)
-                static_assert(!YRT_FIRST_FILTER || spine_len == 2, "the filter records extend two-node spines");
-                auto child_start = [&](size_t n) -> long long {
-                    uint32_t c, st;
-                    memcpy(&c, &nodes[2 * n + 1].w, 4);
-                    memcpy(&st, &nodes[2 * n].w, 4);
-                    return (c & leaf_bit) ? -1 : (long long)(base + st);
-                };
-                const long long l = child_start(x);
-                const long long r = l < 0 ? -1 : l + 1;
-                const long long rl = r < 0 ? -1 : child_start((size_t)r);
-                for (long long q : {l, rl}) {
-                    if (q < 0) {
-                        out.push_back({0, 0, 0, 0});
-                        out.push_back({0, 0, 0, 0});
-                    } else {
-                        out.push_back(nodes[2 * q]);
-                        out.push_back(nodes[2 * q + 1]);
-                    }
-                }
-            }
         }
         return out;
     };
@@ -585,18 +524,13 @@ device_scene* device_scene_create(const scene& scn, int device) {
         const shape& sp = scn.shapes[ist.shp];
         bbox3f rb = {{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
         if (!sp.bvh.nodes.empty()) rb = sp.bvh.nodes[0].bbox;
-        if (winst_rows == 5) {
-            const f4* t = &tinst[tinst.size() - 4];
-            winst.push_back(t[0]);
-            winst.push_back(t[1]);
-            winst.push_back({t[2].x, t[2].y, t[2].z, rb.min.x});
-            winst.push_back({t[3].x, t[3].y, t[3].z, rb.min.y});
-            winst.push_back({rb.min.z, rb.max.x, rb.max.y, rb.max.z});
-        } else {
-            winst.insert(winst.end(), tinst.end() - 4, tinst.end());
-            winst.push_back({rb.min.x, rb.min.y, rb.min.z, 0});
-            winst.push_back({rb.max.x, rb.max.y, rb.max.z, 0});
-        }
+        static_assert(winst_rows == 5, "winst layout (yrt_device.h)");
+        const f4* t = &tinst[tinst.size() - 4];
+        winst.push_back(t[0]);
+        winst.push_back(t[1]);
+        winst.push_back({t[2].x, t[2].y, t[2].z, rb.min.x});
+        winst.push_back({t[3].x, t[3].y, t[3].z, rb.min.y});
+        winst.push_back({rb.min.z, rb.max.x, rb.max.y, rb.max.z});
     }
 
     // ---- materials, lights, textures ----

@@ -24,8 +24,9 @@
 //  * everything that steers the walk is wave-uniform and lives in SGPRs: node
 //    index, lane masks, stack pointer, instance range, shape root/kind;
 //  * the stack lives in three VGPRs used as 64 lane-indexed slots (slot s = lane s):
-//    a push is a compare + three selects, a pop three v_readlane with the stack
-//    pointer as the lane index -- no LDS round trip, no exec-masked store;
+//    a push is three v_writelane (packet_any: a compare + three selects), a pop three
+//    v_readlane with the stack pointer as the lane index -- no LDS round trip, no
+//    exec-masked store;
 //  * every branch is on an SGPR value (no exec-mask divergence in the walk) and the
 //    primitive tests are branchless (the reference's early returns become one
 //    predicate);
@@ -57,44 +58,6 @@ __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p
 // of `old`, every other lane kept; exec is ignored
 extern "C" __device__ int yrt_llvm_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ int writelane(int old, int value, int lane) { return yrt_llvm_writelane(value, lane, old); }
-__device__ __forceinline__ float lane_value(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ float4 lane_value(float4 v, int l) {
-    return {lane_value(v.x, l), lane_value(v.y, l), lane_value(v.z, l), lane_value(v.w, l)};
-}
-
-#ifndef YRT_FEW_LANE_LOADS
-#define YRT_FEW_LANE_LOADS 0
-#endif
-// N consecutive 16-byte records at a wave-uniform address, for every lane. A load
-// that all 64 lanes issue for the same address still costs the vector-memory pipe
-// a full wave's address processing and a 1 KiB data return; here lanes 0..N-1 fetch
-// one record each (one instruction, N active lanes) and v_readlane broadcasts them
-// into SGPRs, which the VALU reads directly as scalar operands.
-template <int N>
-__device__ __forceinline__ void ld_uniform(const f4* p, float4 (&out)[N]) {
-#if YRT_FEW_LANE_LOADS
-    const int lane = __lane_id();
-    float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (lane < N) v = *reinterpret_cast<const float4*>(p + lane);
-#pragma unroll
-    for (int k = 0; k < N; k++) out[k] = lane_value(v, k);
-#else
-    // all N records in flight before anything consumes them; the empty asm pins all
-    // their lanes (no narrowed loads, no .w reload sunk into a later branch)
-#pragma unroll
-    for (int k = 0; k < N; k++) out[k] = *reinterpret_cast<const float4*>(p + k);
-#pragma unroll
-    for (int k = 0; k < N; k += 2) {
-        if (k + 1 < N)
-            asm volatile("" : "+v"(out[k].x), "+v"(out[k].y), "+v"(out[k].z), "+v"(out[k].w), "+v"(out[k + 1].x),
-                         "+v"(out[k + 1].y), "+v"(out[k + 1].z), "+v"(out[k + 1].w));
-        else
-            asm volatile("" : "+v"(out[k].x), "+v"(out[k].y), "+v"(out[k].z), "+v"(out[k].w));
-    }
-#endif
-}
 
 // N consecutive 16-byte records at a wave-uniform address through the scalar data
 // cache into SGPRs (s_load_dwordx4/x8/x16; the scene is read-only for the whole
@@ -121,13 +84,9 @@ __device__ __forceinline__ const f4* sgpr_ptr(const f4* p) {
 
 template <int N>
 __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
-    static_assert(N == 2 || N == 3 || N == 4 || N == 6 || N == 8, "record count");
+    static_assert(N == 3 || N == 4 || N == 6, "record count");
     const f4* p = sgpr_ptr(p_);
-    if constexpr (N == 2) {
-        sgpr8 a;
-        asm volatile("s_load_dwordx8 %0, %1, 0x0\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
-        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1);
-    } else if constexpr (N == 3) {
+    if constexpr (N == 3) {
         sgpr8 a;
         sgpr4 b;
         asm volatile("s_load_dwordx8 %0, %2, 0x0\n s_load_dwordx4 %1, %2, 0x20\n s_waitcnt lgkmcnt(0)"
@@ -138,7 +97,7 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, 0x0\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
-    } else if constexpr (N == 6) {
+    } else {
         sgpr16 a;
         sgpr8 b;
         asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx8 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
@@ -146,33 +105,14 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
                      : "s"(p));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
         out[4] = rec_of(b, 0), out[5] = rec_of(b, 1);
-    } else {
-        sgpr16 a, b;
-        asm volatile("s_load_dwordx16 %0, %2, 0x0\n s_load_dwordx16 %1, %2, 0x40\n s_waitcnt lgkmcnt(0)"
-                     : "=&s"(a), "=&s"(b)
-                     : "s"(p));
-#pragma unroll
-        for (int k = 0; k < 4; k++) out[k] = rec_of(a, k), out[4 + k] = rec_of(b, k);
     }
-}
-
-#ifndef YRT_SCALAR_LOADS
-#define YRT_SCALAR_LOADS 1  // 0: 64-lane vector loads of the shared records (A/B)
-#endif
-template <int N>
-__device__ __forceinline__ void ld_records(const f4* p, float4 (&out)[N]) {
-#if YRT_SCALAR_LOADS
-    ld_scalar<N>(p, out);
-#else
-    ld_uniform<N>(p, out);
-#endif
 }
 
 // the same with the record index applied as an SGPR byte offset of the load itself
 // (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
 template <int N>
 __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
-    static_assert(N == 3 || N == 4 || N == 5 || N == 6 || N == 8, "record count");
+    static_assert(N == 3 || N == 4 || N == 5, "record count");
     const f4* base = sgpr_ptr(base_);
     const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
     if constexpr (N == 3) {
@@ -186,7 +126,7 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
-    } else if constexpr (N == 5) {
+    } else {
         sgpr16 a;
         sgpr4 b;
         asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx4 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
@@ -194,156 +134,86 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
                      : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
         out[4] = rec_of(b, 0);
-    } else if constexpr (N == 6) {
-        sgpr16 a;
-        sgpr8 b;
-        asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx8 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                     : "=&s"(a), "=&s"(b)
-                     : "s"(base), "s"(off));
-        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
-        out[4] = rec_of(b, 0), out[5] = rec_of(b, 1);
-    } else {
-        sgpr16 a, b;
-        asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                     : "=&s"(a), "=&s"(b)
-                     : "s"(base), "s"(off));
-#pragma unroll
-        for (int k = 0; k < 4; k++) out[k] = rec_of(a, k), out[4 + k] = rec_of(b, k);
     }
 }
 
-#ifndef YRT_SOFF
-#define YRT_SOFF 1
-#endif
 // N records at base + index (16-byte units)
 template <int N>
 __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, float4 (&out)[N]) {
-#if YRT_SCALAR_LOADS && YRT_SOFF
-    if constexpr (N == 3 || N == 4 || N == 5 || N == 6 || N == 8) {
-        ld_scalar_at<N>(base, index, out);
-        return;
-    } else
-#endif
-    {
-        ld_records<N>(base + index, out);
-    }
+    ld_scalar_at<N>(base, index, out);
 }
 
 
 // intersect_triangle (scene.cpp:229-263) without branches: the same values in the
 // same order; the early returns become one predicate (a NaN w1/w2/t passes its
-// range checks exactly as it does in the reference)
-#ifndef YRT_TRI_RCP_FIRST
-#define YRT_TRI_RCP_FIRST 1  // the same in the closest-hit walk (A/B: primary -0.9 % with the early exits; +0.6 % before them)
-#endif
-#ifndef YRT_TRI_SKIPSEL
-#define YRT_TRI_SKIPSEL 1  // closest hit: skip a triangle's hit-record selects when no lane hits it
-#endif
-#ifndef YRT_TRI_TFIRST
-#define YRT_TRI_TFIRST 0  // closest hit: test the distance before the barycentrics (A/B: primary +3 %)
-#endif
-#ifndef YRT_TRI_EARLY
-#define YRT_TRI_EARLY 1  // triangle test: leave after w1 when no lane that counts passes it
-#endif
-#ifndef YRT_TRI_EARLY2
-#define YRT_TRI_EARLY2 1  // the same after the second barycentric test (A/B: shadow -1.1 %, primary -0.8 %)
-#endif
-#ifndef YRT_TRI_RCP
-#define YRT_TRI_RCP 1  // 1: the any-hit walk's 1/den as rcp_nr when in range (A/B: shadow -0.8 %)
-#endif
-// `in`: the lanes whose result is used. 1/den is the reference's IEEE division; with RCP,
-// when every such lane has den and 1/den normal (a wave-uniform check), fast_div.h's
-// rcp_nr gives the same bits in three instructions instead of ten. The closest-hit walk
-// does not gain from it (+0.6 %), the any-hit walk does.
-#ifndef YRT_TRI_MASKS
-#define YRT_TRI_MASKS 1  // wave-level exits from one ballot per compare, ANDed on the scalar unit
-#endif
-// `inm`: the same lanes as a wave mask. A ballot of an AND of compares is materialised in a
-// VGPR and compared back (v_cndmask + v_cmp per exit); a ballot of each compare is the
-// compare's own SGPR result, and the ANDs go to the scalar unit.
-template <bool RCP = false, bool TFIRST = false>
+// range checks exactly as it does in the reference).
+//
+// `in`: the lanes whose result is used; `inm`: the same lanes as a wave mask. 1/den is the
+// reference's IEEE division; with RCP, when every such lane has den and 1/den normal (a
+// wave-uniform check), fast_div.h's rcp_nr gives the same bits in three instructions
+// instead of ten. The test leaves early, wave-wide, after the first and after the second
+// barycentric test when no lane that counts passes them (A/B: shadow -1.1 %, primary
+// -0.8 % for the second exit). The exits use one ballot per compare -- the compare's own
+// SGPR result -- and AND them on the scalar unit (a ballot of an AND of compares is
+// materialised in a VGPR and compared back: v_cndmask + v_cmp per exit).
+template <bool RCP = false>
 __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float tmax, vec3f v0, vec3f e1, vec3f e2,
                                            float& t, float& w1, float& w2, bool in, unsigned long long inm) {
     vec3f r = cross(d, e2);
     float den = dot(r, e1);
-#ifdef YRT_EXP_FASTTRI  // timing diagnostic only: approximate reciprocal (results differ)
-    float inv_den = __builtin_amdgcn_rcpf(den);
-#else
     float inv_den;
-    if (!RCP || (YRT_TRI_MASKS ? (ballot(!rcp_nr_ok(den)) & inm) != 0 : ballot(in && !rcp_nr_ok(den)) != 0))
+    if (!RCP || (ballot(!rcp_nr_ok(den)) & inm) != 0)
         inv_den = 1.0f / den;
     else
         inv_den = rcp_nr(den);
-#endif
     vec3f c = o - v0;
-    if constexpr (TFIRST) {
-        // the distance first (the same values; the tests are independent): in a closest-hit
-        // walk most triangles reached late lie beyond the current hit
-        const vec3f s = cross(c, e1);
-        t = dot(s, e2) * inv_den;
-        if (!ballot(in && (den != 0) && !(t < tmin || t > tmax))) {
-            w1 = w2 = 0.0f;
-            return false;
-        }
-        w1 = dot(r, c) * inv_den;
-        w2 = dot(s, d) * inv_den;
-        return (den != 0) & !(w1 < 0 || w1 > 1) & !(w2 < 0.0f || w1 + w2 > 1.0f) & !(t < tmin || t > tmax);
-    }
     w1 = dot(r, c) * inv_den;
     // !(w1 < 0 || w1 > 1) == !(w1 < 0) && !(w1 > 1): a NaN passes both, as in the reference
-    const unsigned long long m1 = YRT_TRI_MASKS ? inm & ballot(den != 0) & ballot(!(w1 < 0)) & ballot(!(w1 > 1)) : 0ull;
-#if YRT_TRI_EARLY
+    const unsigned long long m1 = inm & ballot(den != 0) & ballot(!(w1 < 0)) & ballot(!(w1 > 1));
     // no lane that counts passes the first barycentric test: the rest of the test (half of
     // it) cannot make any of them hit
-    if (YRT_TRI_MASKS ? m1 == 0 : !ballot(in && (den != 0) && !(w1 < 0 || w1 > 1))) {
+    if (m1 == 0) {
         t = w2 = 0.0f;
         return false;
     }
-#endif
     vec3f s = cross(c, e1);
     w2 = dot(s, d) * inv_den;
-#if YRT_TRI_EARLY2
-    if (YRT_TRI_MASKS ? (m1 & ballot(!(w2 < 0.0f)) & ballot(!(w1 + w2 > 1.0f))) == 0
-                      : !ballot(in && (den != 0) && !(w1 < 0 || w1 > 1) && !(w2 < 0.0f || w1 + w2 > 1.0f))) {
+    if ((m1 & ballot(!(w2 < 0.0f)) & ballot(!(w1 + w2 > 1.0f))) == 0) {
         t = 0.0f;
         return false;
     }
-#endif
     t = dot(s, e2) * inv_den;
     return (den != 0) & !(w1 < 0 || w1 > 1) & !(w2 < 0.0f || w1 + w2 > 1.0f) & !(t < tmin || t > tmax);
 }
 
-template <bool ANY, bool COUNT>
-__device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
-                                             work_counts& wc) {
+// ---- any hit on the reference's binary BVH ----
+// intersect_any (scene.cpp:489) as a packet walk: the instrumented (COUNT) pass, which
+// counts the reference's own box/instance/primitive tests, and scenes too deep for the
+// 4-wide walk's stack (device_scene wide_ok). The timed path is packet_occluded_wide2.
+template <bool COUNT>
+__device__ __forceinline__ bool packet_any(const dev_scene_view& S, const ray3& wray, bool valid, work_counts& wc) {
     const int lane = __lane_id();
     const unsigned long long me = 1ull << lane;
     // a NaN tmin/tmax fails every slab test of the reference: such a ray never enters a node
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
     const vec3f wo = wray.o, wd = wray.d;
-    const float tmin = wray.tmin;
-    float tmax = wray.tmax;
+    const float tmin = wray.tmin, tmax = wray.tmax;
     // ray of the current level (local inside an instance); the world inverse direction
     // is recomputed when the walk leaves an instance leaf rather than kept live
     vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
     // per-lane flags are kept as ints (VGPRs): a bool carried around the loop becomes
     // a 64-bit lane mask merged with exec on every back edge (scalar work per step)
     int hit = 0;
-    // closest hit so far: barycentrics w1, w2 only (ew = {1-w1-w2, w1, w2, 0} for every
-    // primitive kind, rebuilt at the end with the reference's arithmetic); its distance
-    // is tmax
-    float hw1 = 0, hw2 = 0;
     // the stack: slot s of each of these VGPRs is lane s
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
-    unsigned long long done = 0;       // lanes out of the walk (any-hit found / NaN tmax)
+    unsigned long long done = 0;       // lanes out of the walk (a hit found)
     unsigned long long inst_mask = 0;  // lanes entering the current instance leaf
-    int level = 0, sp = 0, base = 0, root = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
+    int level = 0, sp = 0, base = 0, root = 0, kind = 0, inst_next = 0, inst_end = 0;
     int node = 0;
     // spine records of the current level (yrt_device.h tpair/spair): node X's record and
-    // those of X's child start+1, its child start+1, ... -- the nodes the reference
-    // tests back to back (test X; push start; pop start+1 and test it; ...) with no
-    // primitive test, and so no tmax change, in between: one fetch serves them all
+    // its child start+1's -- the nodes the reference tests back to back (test X; push
+    // start; pop start+1 and test it) with no primitive test in between
     const f4* pbase = S.tpair;
     unsigned long long mask = live;
     for (;;) {
@@ -354,13 +224,6 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
 #pragma unroll
         for (int j = 0; j < spine_len; j++) pass[j] = box_hit(co, ci, tmin, tmax, rec[2 * j], rec[2 * j + 1]);
         if (COUNT && lane == 0) wc.wnode++;
-#ifdef YRT_EXP_LAT  // diagnostic: one more dependent fetch per step
-        {
-            float4 again[2];
-            ld_records<2>(pbase + spine_record_f4 * (node ^ (int)(mask & 1)), again);
-            asm volatile("" ::"v"(again[0].x));
-        }
-#endif
         // walk down the spine: node j is tested by the lanes that passed node j-1
         int lstart = 0;          // the leaf to process after this step, if any:
         uint32_t lcl = 0;        //   first slot, count | leaf_bit,
@@ -407,39 +270,28 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                 const bool in = (lmask >> lane) & 1;
                 int leaf_hit = 0;
                 for (int i = start; i < start + count; i++) {
-                    const f4* pr = S.sprims + 3 * i;
                     float4 pv[3];
-                    ld_records<3>(pr, pv);
+                    ld_scalar<3>(S.sprims + 3 * i, pv);
                     const float4 a = pv[0], b = pv[1], c = pv[2];
-                    if (COUNT && in && !(ANY && leaf_hit)) wc.prim++;
+                    if (COUNT && in && !leaf_hit) wc.prim++;
                     if (COUNT && lane == 0) wc.wprim++;
                     float t, w1, w2;
                     bool h;
                     if (kind == kind_triangles) {
                         h = tri_hit_nb(co, cd, tmin, tmax, xyz(a), xyz(b), xyz(c), t, w1, w2, in, ballot(in));
                     } else {
-                        // lines: ew = {1-s, s, 0, 0}; points: {1, 0, 0, 0} -- both are
-                        // {1-w1-w2, w1, w2, 0} with w1 = ew.y, w2 = ew.z
                         vec4f ew;
                         const ray3 lr = {co, cd, tmin, tmax};
                         h = kind == kind_lines ? line_hit(lr, xyz(a), xyz(b), b.w, c.x, t, ew)
                                                : point_hit(lr, xyz(a), b.x, t, ew);
-                        w1 = ew.y, w2 = ew.z;
                     }
                     h = h && in;
-                    if (!ANY) {
-                        tmax = h ? t : tmax;
-                        hr.slot = h ? cur_slot : hr.slot;
-                        hr.ei = h ? ibits(a.w) : hr.ei;
-                        hw1 = h ? w1 : hw1;
-                        hw2 = h ? w2 : hw2;
-                    }
                     leaf_hit |= h ? 1 : 0;
                 }
-                if (ANY) hit |= leaf_hit;  // closest hit: hit == (hr.slot >= 0), nothing to carry
-                // any-hit lanes are finished; a NaN tmax fails every later slab test
-                done |= ballot(ANY ? leaf_hit : (leaf_hit && is_nan(tmax)));
-                if (ANY && !(live & ~done)) return hit;
+                hit |= leaf_hit;
+                // lanes with a hit are finished
+                done |= ballot(leaf_hit);
+                if (!(live & ~done)) return hit;
             }
         }
         // ---- next: the next instance of the current leaf, or pop ----
@@ -448,9 +300,8 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                 if (inst_next < inst_end) {
                     // enter instance k: transform_ray_inverse (vmath.h:275-278), every lane
                     const int k = inst_next++;
-                    const f4* ti = S.tinst + 4 * k;
                     float4 fr[4];
-                    ld_records<4>(ti, fr);
+                    ld_scalar<4>(S.tinst + 4 * k, fr);
                     const float4 fx = fr[0], fy = fr[1], fz = fr[2], fo = fr[3];
                     const frame3f f = {xyz(fx), xyz(fy), xyz(fz), xyz(fo)};
                     co = transform_point_inverse(f, wo);
@@ -460,7 +311,6 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                     root = (int)(rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
                     pbase = S.spair + spine_record_f4 * root;
-                    cur_slot = k;
                     node = 0;  // the shape root, tested like any popped node
                     mask = inst_mask & ~done;
                     if (COUNT && (mask & me)) wc.inst++;
@@ -473,15 +323,7 @@ __device__ __forceinline__ bool packet_trace(const dev_scene_view& S, const ray3
                 cd = wd;
                 ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
             }
-            if (sp == 0) {
-                if (!ANY) {
-                    if (hr.slot < 0) return false;
-                    hr.ew = {1 - hw1 - hw2, hw1, hw2, 0};
-                    hr.dist = tmax;
-                    return true;
-                }
-                return hit;
-            }
+            if (sp == 0) return hit;
             sp--;
             node = __builtin_amdgcn_readlane(stk_node, sp);
             const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp);
@@ -520,58 +362,37 @@ static __device__ unsigned long long g_wide_stats[1024 * 16];
 #define WSTAT(i, v) ((void)0)
 #endif
 
-#ifndef YRT_FAST_DIV
-#define YRT_FAST_DIV 1
-#endif
-#ifndef YRT_FAST_SQRT
-#define YRT_FAST_SQRT 1  // instance entry: normalize's sqrt as sqrt_nr when every lane admits it
-#endif
-
 // the instance-local direction and its inverse on instance entry (transform_ray_inverse,
 // vmath.h:275-278: the direction renormalized, invd = 1/d as intersect_check_bbox
-// computes it). YRT_EXP_FASTINST is a timing diagnostic only (approximate rcp/rsqrt,
-// results differ): it prices the exact math of an instance entry.
+// computes it).
 //
 // The four reciprocals (normalize's 1/l, vmath.h:118-122, and invd) are exact IEEE
-// divisions in the reference. With YRT_FAST_DIV they are rcp_nr (fast_div.h: v_rcp_f32
+// divisions in the reference. Here they are rcp_nr (fast_div.h: v_rcp_f32
 // plus one Newton step, bit-identical to 1.0f / x on every input it admits -- checked on
 // all 2^32 floats) whenever every live lane's l and cd components are in the normal range;
 // otherwise (a zero, subnormal, huge, infinite or NaN value in some lane) the wave takes
 // the division.
 __device__ __forceinline__ void enter_direction(const frame3f& f, vec3f wd, unsigned long long lanes, vec3f& cd,
                                                 vec3f& ci) {
-#ifdef YRT_EXP_FASTINST
-    const vec3f v = {dot(f.x, wd), dot(f.y, wd), dot(f.z, wd)};
-    const float r = __builtin_amdgcn_rsqf(dot(v, v));
-    cd = {v.x * r, v.y * r, v.z * r};
-    ci = {__builtin_amdgcn_rcpf(cd.x), __builtin_amdgcn_rcpf(cd.y), __builtin_amdgcn_rcpf(cd.z)};
-#else
-#if YRT_FAST_DIV
     {
         const vec3f v = {dot(f.x, wd), dot(f.y, wd), dot(f.z, wd)};
         const float l2 = dot(v, v);  // length(v) = sqrt(dot(v, v))
-        const float l = YRT_FAST_SQRT ? sqrt_nr(l2) : __builtin_sqrtf(l2);
+        const float l = sqrt_nr(l2);  // normalize's sqrt; exact where sqrt_nr_ok (fast_div.h)
         const float y = rcp_nr(l);
         const vec3f c = v * y;
         const float lo = fminf(fminf(l, fabsf(c.x)), fminf(fabsf(c.y), fabsf(c.z)));
         const float hi = fmaxf(fmaxf(l, fabsf(c.x)), fmaxf(fabsf(c.y), fabsf(c.z)));
         // l == l: a NaN component makes l NaN (fminf/fmaxf would drop it)
-        const bool fast = (l == l) && lo >= 0x1p-126f && hi < 0x1p126f && (!YRT_FAST_SQRT || sqrt_nr_ok(l2));
+        const bool fast = (l == l) && lo >= 0x1p-126f && hi < 0x1p126f && sqrt_nr_ok(l2);
         if (!(ballot(!fast) & lanes)) {
             cd = c;
             ci = {rcp_nr(c.x), rcp_nr(c.y), rcp_nr(c.z)};
             return;
         }
     }
-#endif
     cd = transform_direction_inverse(f, wd);
     ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
-#endif
 }
-
-#ifndef YRT_WIDE_OCTANT
-#define YRT_WIDE_OCTANT 1  // wave-uniform slab signs: near/far planes picked at compile time
-#endif
 
 // intersect_check_bbox (scene.cpp:371-382) with the per-axis swap decided at compile
 // time: OCT bit a set = this lane's invd component a is < 0 (the reference's swap
@@ -597,60 +418,6 @@ __device__ __forceinline__ bool box_oct(vec3f o, vec3f invd, float tmin_r, float
     }
 }
 
-#ifndef YRT_PK_BOX
-#define YRT_PK_BOX 0  // wide walk: two children's slab products per packed-f32 instruction (A/B: shadow +5.3 %)
-#endif
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// box_oct<OCT> for two children at once (OCT < 8). Each (n - o) * invd product is one
-// lane of a v_pk_add_f32 / v_pk_mul_f32 (the children's planes are adjacent SGPRs of
-// the wide record), so the twelve subtractions and twelve products of two slab tests
-// take twelve instructions instead of twenty-four. Packed f32 arithmetic rounds every
-// lane as the scalar instruction does (IEEE, same denormal mode), so each product, and
-// the min/max chain below that is box_oct's, is bit-identical.
-template <int OCT>
-__device__ __forceinline__ void box_oct_pair(vec3f o, vec3f invd, float tmin_r, float tmax_r, f2v lx, f2v ly, f2v lz,
-                                             f2v hx, f2v hy, f2v hz, bool& p0, bool& p1) {
-    static_assert(OCT >= 0 && OCT < 8, "box_oct_pair is for a shared octant");
-    const f2v nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
-    const f2v ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
-    const f2v nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
-    const f2v ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const f2v ix = {invd.x, invd.x}, iy = {invd.y, invd.y}, iz = {invd.z, invd.z};
-    const f2v t0x = (nx - ox) * ix, t0y = (ny - oy) * iy, t0z = (nz - oz) * iz;
-    const f2v t1x = (fx - ox) * ix, t1y = (fy - oy) * iy, t1z = (fz - oz) * iz;
-    const float tmin0 = fmaxf(fmaxf(fmaxf(t0x.x, t0y.x), t0z.x), tmin_r);
-    const float tmin1 = fmaxf(fmaxf(fmaxf(t0x.y, t0y.y), t0z.y), tmin_r);
-    f2v tmax = {fminf(fminf(fminf(t1x.x, t1y.x), t1z.x), tmax_r), fminf(fminf(fminf(t1x.y, t1y.y), t1z.y), tmax_r)};
-    tmax *= f2v{1.00000024f, 1.00000024f};
-    p0 = tmin0 <= tmax.x;
-    p1 = tmin1 <= tmax.y;
-}
-
-#ifndef YRT_PK_BOX_FIRST
-#define YRT_PK_BOX_FIRST 0  // closest-hit walk: each box's x and y slab products packed (A/B: primary +3.3 %)
-#endif
-
-// box_oct<OCT> for one box with its x and y planes packed: (lo.x, lo.y) and (hi.x, hi.y)
-// are adjacent SGPRs of the spine record, so the x/y products of both planes take two
-// v_pk_add_f32 and two v_pk_mul_f32 (z stays scalar). Each lane rounds as the scalar
-// instruction does, so every product, and the result, is box_oct's bit for bit.
-template <int OCT>
-__device__ __forceinline__ bool box_oct_xy(vec3f o, vec3f invd, float tmin_r, float tmax_r, f2v lxy, float lz, f2v hxy,
-                                           float hz) {
-    static_assert(OCT >= 0 && OCT < 8, "box_oct_xy is for a shared octant");
-    const f2v oxy = {o.x, o.y}, ixy = {invd.x, invd.y};
-    const f2v tl = (lxy - oxy) * ixy, th = (hxy - oxy) * ixy;
-    const float tlz = (lz - o.z) * invd.z, thz = (hz - o.z) * invd.z;
-    const float t0x = (OCT & 1) ? th.x : tl.x, t1x = (OCT & 1) ? tl.x : th.x;
-    const float t0y = (OCT & 2) ? th.y : tl.y, t1y = (OCT & 2) ? tl.y : th.y;
-    const float t0z = (OCT & 4) ? thz : tlz, t1z = (OCT & 4) ? tlz : thz;
-    float tmin = fmaxf(fmaxf(fmaxf(t0x, t0y), t0z), tmin_r);
-    float tmax = fminf(fminf(fminf(t1x, t1y), t1z), tmax_r);
-    tmax *= 1.00000024f;
-    return tmin <= tmax;
-}
-
 // the octant shared by every lane of `lanes` (bit a: invd component a < 0), or 8
 __device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes) {
     const unsigned long long nx = ballot(invd.x < 0) & lanes, ny = ballot(invd.y < 0) & lanes,
@@ -658,10 +425,6 @@ __device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes)
     if ((nx && nx != lanes) || (ny && ny != lanes) || (nz && nz != lanes)) return 8;
     return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
 }
-
-#ifndef YRT_INNER_POP
-#define YRT_INNER_POP 1  // descents pop inside their octant's loop (no re-dispatch per pop)
-#endif
 
 // pop inside a descent: entries above `floor` until one with live lanes (true), or down
 // to the floor (false, mask 0) -- the level boundary is the caller's
@@ -679,68 +442,37 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
     return false;
 }
 
-#ifndef YRT_WI_LDS
-#define YRT_WI_LDS 1  // closest hit: the world 1/d kept in LDS across instance leaves (A/B: primary -1 %)
-#endif
 constexpr int packet_block = 256;  // >= threads per block of every kernel that runs packet_first
 
-#ifndef YRT_FIRST_HOIST
-#define YRT_FIRST_HOIST 1  // closest-hit descent: the record base made wave-uniform once per descent
-#endif
-#ifndef YRT_IDENT_INST
-#define YRT_IDENT_INST 1  // instances with an identity rotation share one instance-local direction per walk
-#endif
-#ifndef YRT_FIRST_OCTANT
-#define YRT_FIRST_OCTANT 1  // closest hit: octant-specialised slab tests (see box_oct)
-#endif
 
 // one descent of the closest-hit walk from the spine record at byte offset `node` of
 // pbase: returns with mask = 0 when no lane passes, or with a leaf reached (mask: its
 // lanes, node: its first slot, cl: count | leaf_bit). Per spine node: one ballot &
-// mask, one leaf test, one push (v_writelane of the record offset and lane mask).
+// mask, one leaf test, one push (v_writelane of the record offset and lane mask). A
+// node no lane passes pops inside the descent (no re-dispatch of the octant copy).
 template <int OCT, bool COUNT>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
                                               work_counts& wc, int floor, unsigned long long done) {
-    constexpr bool FILTER = YRT_FIRST_FILTER && !COUNT;  // the instrumented pass counts the reference's tests
-#if YRT_FIRST_HOIST
     const f4* pb = sgpr_ptr(pbase);  // once per descent, not per record (the compiler kept pbase in VGPRs)
-#else
-#define pb sgpr_ptr(pbase)
-#endif
     for (;;) {
-        float4 rec[FILTER ? 8 : 4];
-        if constexpr (FILTER) {
-            sgpr16 a, b;
-            asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                         : "=&s"(a), "=&s"(b)
-                         : "s"(pb), "s"(uniform(node)));
-#pragma unroll
-            for (int k = 0; k < 4; k++) rec[k] = rec_of(a, k), rec[4 + k] = rec_of(b, k);
-        } else {
+        float4 rec[4];
+        {
             sgpr16 a;
             asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
                          : "=s"(a)
                          : "s"(pb), "s"(uniform(node)));
             rec[0] = rec_of(a, 0), rec[1] = rec_of(a, 1), rec[2] = rec_of(a, 2), rec[3] = rec_of(a, 3);
         }
-        bool p0, p1;
-        if constexpr (YRT_PK_BOX_FIRST && OCT < 8) {
-            p0 = box_oct_xy<OCT>(co, ci, tmin, tmax, f2v{rec[0].x, rec[0].y}, rec[0].z, f2v{rec[1].x, rec[1].y}, rec[1].z);
-            p1 = box_oct_xy<OCT>(co, ci, tmin, tmax, f2v{rec[2].x, rec[2].y}, rec[2].z, f2v{rec[3].x, rec[3].y}, rec[3].z);
-        } else {
-            p0 = box_oct<OCT>(co, ci, tmin, tmax, rec[0].x, rec[0].y, rec[0].z, rec[1].x, rec[1].y, rec[1].z);
-            p1 = box_oct<OCT>(co, ci, tmin, tmax, rec[2].x, rec[2].y, rec[2].z, rec[3].x, rec[3].y, rec[3].z);
-        }
+        const bool p0 = box_oct<OCT>(co, ci, tmin, tmax, rec[0].x, rec[0].y, rec[0].z, rec[1].x, rec[1].y, rec[1].z);
+        const bool p1 = box_oct<OCT>(co, ci, tmin, tmax, rec[2].x, rec[2].y, rec[2].z, rec[3].x, rec[3].y, rec[3].z);
         if (COUNT && (me & 1)) wc.wnode++;
         if (COUNT && (mask & me)) wc.box++;
         const unsigned long long pm0 = ballot(p0) & mask;
         mask = pm0;
         if (!pm0) {
-#if YRT_INNER_POP
             if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
-#endif
             return;
         }
         const int s0 = uniform(ibits(rec[0].w));
@@ -749,27 +481,16 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
             node = s0, cl = c0;
             return;
         }
-        {
-            // push L (X's child start) for the lanes that passed X; with the filter, only
-            // those that also pass L's box now (its reference test at the pop uses a
-            // tmax no larger than the current one, and the test is monotone in tmax)
-            unsigned long long pl = pm0;
-            if constexpr (FILTER)
-                pl &= ballot(box_oct<OCT>(co, ci, tmin, tmax, rec[4].x, rec[4].y, rec[4].z, rec[5].x, rec[5].y, rec[5].z));
-            if (!FILTER || pl) {
-                stk_node = writelane(stk_node, s0, sp);
-                stk_mlo = writelane(stk_mlo, (int)(uint32_t)pl, sp);
-                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pl >> 32), sp);
-                sp++;
-            }
-        }
+        // push L (X's child start) for the lanes that passed X
+        stk_node = writelane(stk_node, s0, sp);
+        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
+        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
+        sp++;
         if (COUNT && (pm0 & me)) wc.box++;
         const unsigned long long pm1 = ballot(p1) & pm0;
         mask = pm1;
         if (!pm1) {
-#if YRT_INNER_POP
             if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
-#endif
             return;
         }
         const int s1 = uniform(ibits(rec[2].w));
@@ -778,28 +499,19 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
             node = s1, cl = c1;
             return;
         }
-        {
-            unsigned long long prl = pm1;  // RL (R's child start), filtered the same way
-            if constexpr (FILTER)
-                prl &= ballot(box_oct<OCT>(co, ci, tmin, tmax, rec[6].x, rec[6].y, rec[6].z, rec[7].x, rec[7].y, rec[7].z));
-            if (!FILTER || prl) {
-                stk_node = writelane(stk_node, s1, sp);
-                stk_mlo = writelane(stk_mlo, (int)(uint32_t)prl, sp);
-                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(prl >> 32), sp);
-                sp++;
-            }
-        }
+        // push RL (R's child start)
+        stk_node = writelane(stk_node, s1, sp);
+        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
+        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
+        sp++;
         node = s1 + spine_record_bytes;
     }
-#if !YRT_FIRST_HOIST
-#undef pb
-#endif
 }
 
 // ---- closest hit, laid out for the scalar unit ----
-// The same walk as packet_trace<false> (same node tests, in the same order, with the
-// same tmax per lane), with the control flow written as explicit states joined by
-// gotos so that the hot descent path carries no merged loop state: per spine node
+// The packet discipline of packet_any (same node tests, in the reference's order, with
+// the same tmax per lane), with the control flow written so that the hot descent path
+// carries no merged loop state: per spine node
 // one s_and (ballot & mask, SCC = any lane), one leaf test and one stack push. The
 // push is three v_writelane of the SGPR values into lane sp of the stack VGPRs (no
 // lane-index compare, no selects). SALU issue -- one scalar unit per CU shared by
@@ -816,12 +528,10 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     const float tmin = wray.tmin;
     float tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
-#if YRT_WI_LDS
     // the world inverse direction, parked in LDS for the returns from instance leaves
     // (three ds_read instead of three IEEE divisions; three VGPRs stay free)
     __shared__ float wi_lds[3][packet_block];
     wi_lds[0][threadIdx.x] = ci.x, wi_lds[1][threadIdx.x] = ci.y, wi_lds[2][threadIdx.x] = ci.z;
-#endif
     float hw1 = 0, hw2 = 0;
     int hslot = -1, hei = -1;
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
@@ -829,15 +539,15 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
     int node = 0;  // byte offset of the current spine record from pbase
     const f4* pbase = S.tpair;
-    const int woct = YRT_FIRST_OCTANT ? wave_octant(ci, live) : 8;
+    // the octant of the current level's rays when the whole wave shares it (8: mixed):
+    // the descent runs the copy with its slab swaps resolved at compile time (box_oct)
+    const int woct = wave_octant(ci, live);
     int oct = woct;
-#if YRT_IDENT_INST
     // the instance-local direction of the instances with an identity rotation, once per
     // walk (packet_occluded_wide2 does the same)
     vec3f icd, ici;
     enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
-    const int ioct = YRT_FIRST_OCTANT ? wave_octant(ici, live) : 8;
-#endif
+    const int ioct = wave_octant(ici, live);
     for (;;) {
         // ---- descent: one spine record per step, until a leaf or no passing lane ----
         DBG_CHECK(node >= 0 && (node % spine_record_bytes) == 0 && sp >= 0 && sp < 63 &&
@@ -848,7 +558,6 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
         const int floor = level ? base : 0;
 #define YRT_FD(o) \
     first_descend<o, COUNT>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc, floor, done)
-#if YRT_FIRST_OCTANT
         switch (oct) {
             case 0: YRT_FD(0); break;
             case 1: YRT_FD(1); break;
@@ -860,9 +569,6 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
             case 7: YRT_FD(7); break;
             default: YRT_FD(8); break;
         }
-#else
-        YRT_FD(8);
-#endif
 #undef YRT_FD
         const unsigned long long lmask = mask;
         const int lstart = node, lcount = (int)(lcl & 0xffffu);
@@ -885,12 +591,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                         if (COUNT && in) wc.prim++;
                         if (COUNT && (me & 1)) wc.wprim++;
                         float t, w1, w2;
-                        const bool h =
-                            tri_hit_nb<YRT_TRI_RCP_FIRST, YRT_TRI_TFIRST>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]),
-                                                                          xyz(pv[2]), t, w1, w2, in, lmask) &&
-                            in;
+                        const bool h = tri_hit_nb<true>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t,
+                                                        w1, w2, in, lmask) &&
+                                       in;
                         // most triangles hit no lane: their record-keeping selects are skipped
-                        if (!YRT_TRI_SKIPSEL || ballot(h)) {
+                        if (ballot(h)) {
                             tmax = h ? t : tmax;
                             hslot = h ? cur_slot : hslot;
                             hei = h ? ibits(pv[0].w) : hei;
@@ -937,12 +642,10 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-#if YRT_IDENT_INST
                     const bool ident = (uniform(ibits(fr[0].w)) & (int)inst_identity_bit) != 0;
                     if (ident)
                         cd = icd, ci = ici;
                     else
-#endif
                         enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[3].w));
                     pbase = S.spair + spine_record_f4 * (rk & 0x3fffffffu);
@@ -951,11 +654,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     mask = inst_mask & ~done;
                     if (COUNT && (mask & me)) wc.inst++;
                     node = 0;  // the shape root, tested like any popped node
-#if YRT_IDENT_INST
-                    if (YRT_FIRST_OCTANT) oct = ident ? ioct : wave_octant(ci, live & ~done);
-#else
-                    if (YRT_FIRST_OCTANT) oct = wave_octant(ci, live & ~done);
-#endif
+                    oct = ident ? ioct : wave_octant(ci, live & ~done);
                     if (mask) break;
                     continue;
                 }
@@ -963,11 +662,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 pbase = S.tpair;
                 co = wo;
                 cd = wd;
-#if YRT_WI_LDS
                 ci = {wi_lds[0][threadIdx.x], wi_lds[1][threadIdx.x], wi_lds[2][threadIdx.x]};
-#else
-                ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
-#endif
                 oct = woct;
             }
             if (sp == 0) {
@@ -991,46 +686,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     return true;
 }
 
-#ifndef YRT_LEAF_EARLY
-#define YRT_LEAF_EARLY 0  // any hit: leave a leaf once every lane in it is occluded
-#endif
-
-#ifndef YRT_WIDE_SWITCH
-#define YRT_WIDE_SWITCH 0  // any hit: the passing children pushed by one switch on their 4-bit pattern (A/B: shadow +2.2 %; the switch compiles to a compare tree)
-#endif
-#ifndef YRT_WIDE_PUSHALL
-#define YRT_WIDE_PUSHALL 0  // wide step: every slot written to the stack, sp advanced per passing slot, top popped (A/B: shadow +6.8 %)
-#endif
-#ifndef YRT_WIDE_ASMSEL
-#define YRT_WIDE_ASMSEL 1  // wide step: the passing-slot selection and pushes as one scalar asm block
-#endif
-#ifndef YRT_WIDE_ROOTBOX
-#define YRT_WIDE_ROOTBOX 1  // any hit: a shape's root box tested on entering an instance
-#endif
-#ifndef YRT_WIDE_SKIP
-#define YRT_WIDE_SKIP 1  // 1: scalar branch around a node's empty slots; 0: test all four
-#endif
-
-#ifndef YRT_APRIMS
-#define YRT_APRIMS 1  // any hit: triangles from the packed 9-float array (aprims)
-#endif
-#ifndef YRT_WIDE_R7
-#define YRT_WIDE_R7 0  // 1: a wide step loads the record's last row (its slot count) too
-#endif
-
-// A wide record through the scalar cache. Without YRT_WIDE_R7 only its first 112 bytes
-// (bounds and child words: x16 + x8 + x4, 28 SGPRs instead of 32) -- the slot count in the
-// last row is implied by the child words, an empty slot's word being wide_leaf exactly (a
-// leaf of no primitives: skipping one changes nothing).
-__device__ __forceinline__ void ld_wide_record(const f4* wbase, uint32_t off, float4 (&r)[8]) {
-#if YRT_WIDE_R7
-    sgpr16 a, b;
-    asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx16 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
-                 : "=&s"(a), "=&s"(b)
-                 : "s"(wbase), "s"(uniform((int)off)));
-#pragma unroll
-    for (int k = 0; k < 4; k++) r[k] = rec_of(a, k), r[4 + k] = rec_of(b, k);
-#else
+// A wide record through the scalar cache: its first 112 bytes (bounds and child words:
+// x16 + x8 + x4, 28 SGPRs instead of 32) -- the slot count in the last row is implied by
+// the child words, an empty slot's word being wide_leaf exactly (a leaf of no
+// primitives: skipping one changes nothing). A/B: shadow -1.1 to -1.7 %.
+__device__ __forceinline__ void ld_wide_record(const f4* wbase, uint32_t off, float4 (&r)[7]) {
     sgpr16 a;
     sgpr8 b;
     sgpr4 c;
@@ -1042,46 +702,25 @@ __device__ __forceinline__ void ld_wide_record(const f4* wbase, uint32_t off, fl
 #pragma unroll
     for (int k = 0; k < 4; k++) r[k] = rec_of(a, k);
     r[4] = rec_of(b, 0), r[5] = rec_of(b, 1), r[6] = rec_of(c, 0);
-    r[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#endif
 }
 
 // the slab tests of a wide step on the record r: m[k] = the lanes of `mask` that pass
-// slot k's box (0 for a slot the node does not have), w[k] = slot k's child word
+// slot k's box (0 for a slot the node does not have: a scalar branch around it), w[k] =
+// slot k's child word
 template <int OCT>
-__device__ __forceinline__ void wide_tests(const float4 (&r)[8], vec3f co, vec3f ci, float tmin, float tmax,
+__device__ __forceinline__ void wide_tests(const float4 (&r)[7], vec3f co, vec3f ci, float tmin, float tmax,
                                            unsigned long long mask, uint32_t (&w)[4], unsigned long long (&m)[4]) {
     const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
                 lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
                 hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
     w[0] = (uint32_t)uniform(ibits(r[6].x)), w[1] = (uint32_t)uniform(ibits(r[6].y));
     w[2] = (uint32_t)uniform(ibits(r[6].z)), w[3] = (uint32_t)uniform(ibits(r[6].w));
-    // whether slot k (k >= 2) exists: the record's slot count, or its child word
-    auto has = [&](int k) { return YRT_WIDE_R7 ? k < uniform(ibits(r[7].x)) : w[k] != wide_leaf; };
-    if constexpr (YRT_PK_BOX && OCT < 8) {
-        // slots 0 and 1 always (a leaf root's empty slot 1 fails its test), 2 and 3
-        // when the node has a third slot; a missing fourth is masked out
-        bool p0, p1;
-        box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[0], lx[1]}, f2v{ly[0], ly[1]}, f2v{lz[0], lz[1]},
-                          f2v{hx[0], hx[1]}, f2v{hy[0], hy[1]}, f2v{hz[0], hz[1]}, p0, p1);
-        m[0] = ballot(p0) & mask;
-        m[1] = ballot(p1) & mask;
-        m[2] = m[3] = 0;
-        if (has(2)) {
-            bool p2, p3;
-            box_oct_pair<OCT>(co, ci, tmin, tmax, f2v{lx[2], lx[3]}, f2v{ly[2], ly[3]}, f2v{lz[2], lz[3]},
-                              f2v{hx[2], hx[3]}, f2v{hy[2], hy[3]}, f2v{hz[2], hz[3]}, p2, p3);
-            m[2] = ballot(p2) & mask;
-            m[3] = has(3) ? ballot(p3) & mask : 0ull;
-        }
-    } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (!YRT_WIDE_SKIP || k < 2 || has(k))  // every wide node has >= 2 slots but a leaf root's 1
-                m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
-            else
-                m[k] = 0;
-        }
+    for (int k = 0; k < 4; k++) {
+        if (k < 2 || w[k] != wide_leaf)  // every wide node has >= 2 slots but a leaf root's 1
+            m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
+        else
+            m[k] = 0;
     }
 }
 
@@ -1091,7 +730,7 @@ __device__ __forceinline__ void wide_tests(const float4 (&r)[8], vec3f co, vec3f
 // passing ones are pushed last-to-first (three v_writelane each: word, mask halves), so
 // they pop in slot order. Returns true to continue the descent from `cur`.
 template <int OCT>
-__device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f ci, float tmin, float tmax,
+__device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f ci, float tmin, float tmax,
                                           uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
                                           int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
     uint32_t w[4];
@@ -1099,36 +738,6 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
     wide_tests<OCT>(r, co, ci, tmin, tmax, mask, w, m);
     unsigned long long cm = 0;
     uint32_t cw = 0;
-#if YRT_WIDE_SWITCH
-    // the passing slots as four bits, then one straight-line case per pattern: the lowest
-    // passing slot becomes current, the others are pushed highest first (so they pop in
-    // slot order) at lanes sp, sp+1, ... -- no compare per slot after the bits
-    auto push = [&](int k, int at) {
-        stk_word = writelane(stk_word, (int)w[k], sp + at);
-        stk_mlo = writelane(stk_mlo, (int)(uint32_t)m[k], sp + at);
-        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m[k] >> 32), sp + at);
-    };
-    const unsigned bits = (m[0] ? 1u : 0u) | (m[1] ? 2u : 0u) | (m[2] ? 4u : 0u) | (m[3] ? 8u : 0u);
-    switch (bits) {
-        case 0: cm = 0; cw = 0; break;
-        case 1: cm = m[0]; cw = w[0]; break;
-        case 2: cm = m[1]; cw = w[1]; break;
-        case 3: push(1, 0); sp += 1; cm = m[0]; cw = w[0]; break;
-        case 4: cm = m[2]; cw = w[2]; break;
-        case 5: push(2, 0); sp += 1; cm = m[0]; cw = w[0]; break;
-        case 6: push(2, 0); sp += 1; cm = m[1]; cw = w[1]; break;
-        case 7: push(2, 0); push(1, 1); sp += 2; cm = m[0]; cw = w[0]; break;
-        case 8: cm = m[3]; cw = w[3]; break;
-        case 9: push(3, 0); sp += 1; cm = m[0]; cw = w[0]; break;
-        case 10: push(3, 0); sp += 1; cm = m[1]; cw = w[1]; break;
-        case 11: push(3, 0); push(1, 1); sp += 2; cm = m[0]; cw = w[0]; break;
-        case 12: push(3, 0); sp += 1; cm = m[2]; cw = w[2]; break;
-        case 13: push(3, 0); push(2, 1); sp += 2; cm = m[0]; cw = w[0]; break;
-        case 14: push(3, 0); push(2, 1); sp += 2; cm = m[1]; cw = w[1]; break;
-        case 15: push(3, 0); push(2, 1); push(1, 2); sp += 3; cm = m[0]; cw = w[0]; break;
-        default: break;
-    }
-#elif YRT_WIDE_ASMSEL
     // the select chain as written for the scalar unit. Chain A tests the slots from the
     // highest while none has passed; the first passing slot j becomes the candidate and
     // control moves to the blocks that know it: B(j,k) tests slot k < j and, when it
@@ -1234,42 +843,9 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
         cw = (uint32_t)uniform((int)ow);
         cm = (unsigned long long)(uint32_t)uniform((int)(om >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)om);
     }
-#else
-#pragma unroll
-    for (int k = 3; k >= 0; k--) {
-        if (m[k]) {
-            if (cm) {
-                stk_word = writelane(stk_word, (int)cw, sp);
-                stk_mlo = writelane(stk_mlo, (int)(uint32_t)cm, sp);
-                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(cm >> 32), sp);
-                sp++;
-            }
-            cm = m[k];
-            cw = w[k];
-        }
-    }
-#endif
     mask = cm;
     cur = cw;
-#ifdef YRT_EXP_SALU  // sensitivity diagnostic: N extra SALU per wide step (A/B: +8 -> shadow +3.4 %)
-    {
-        int d;
-        asm volatile("s_mov_b32 %0, 0" : "=s"(d));
-#pragma unroll
-        for (int q = 0; q < YRT_EXP_SALU; q++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d) : : "scc");
-        asm volatile("" ::"s"(d));
-    }
-#endif
-#ifdef YRT_EXP_VALU  // sensitivity diagnostic: N extra VALU per wide step (A/B: +8 -> shadow +2.2 %)
-    {
-        float d = co.x;
-#pragma unroll
-        for (int q = 0; q < YRT_EXP_VALU; q++) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
-        asm volatile("" ::"v"(d));
-    }
-#endif
     if (cm) return !(cw & wide_leaf);
-#if YRT_INNER_POP
     {
         int n = 0;
         if (inner_pop(floor, done, n, mask, sp, stk_word, stk_mlo, stk_mhi)) {
@@ -1277,7 +853,6 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[8], vec3f co, vec3f 
             return !(cur & wide_leaf);
         }
     }
-#endif
     return false;
 }
 
@@ -1292,82 +867,19 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, const floa
                                              int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
                                              unsigned long long done, unsigned& nsteps) {
     const f4* wbase = sgpr_ptr(S.wnodes);
-#if YRT_WIDE_PUSHALL
-    // every slot is written to stack lane sp, highest first, and sp advances past each
-    // one with live lanes (s_cmp_lg_u64 + s_addc_u32, no branch per slot); then the top
-    // entry is popped: the lowest passing slot if any passed (it pops first, as the
-    // select chain's current item would), else the entry below -- the pop the walk makes
-    // next anyway. One asm block: M0 carries sp (a v_writelane takes its lane select from
-    // M0 so that the data SGPR is its one constant-bus read). Absent slots have m = 0.
-    for (;;) {
-#ifdef YRT_WIDE_STATS
-        nsteps++;
-#endif
-        float4 r[8];
-        if (LDSN > 0 && cur < (uint32_t)(LDSN * wide_record_bytes)) {
-            const float4* p = lds + (cur >> 4);
-#pragma unroll
-            for (int k = 0; k < 8; k++) r[k] = p[k];
-        } else {
-            ld_wide_record(wbase, cur, r);
-        }
-        uint32_t w[4];
-        unsigned long long m[4];
-        wide_tests<OCT>(r, co, ci, tmin, tmax, mask, w, m);
-        int spn;
-        uint32_t cw, ml, mh;
-        asm volatile(
-            "s_mov_b32 m0, %[sp]\n"
-            "v_writelane_b32 %[sw], %[w3], m0\n v_writelane_b32 %[sl], %[l3], m0\n v_writelane_b32 %[sh], %[h3], m0\n"
-            "s_cmp_lg_u64 %[m3], 0\n s_addc_u32 m0, m0, 0\n"
-            "v_writelane_b32 %[sw], %[w2], m0\n v_writelane_b32 %[sl], %[l2], m0\n v_writelane_b32 %[sh], %[h2], m0\n"
-            "s_cmp_lg_u64 %[m2], 0\n s_addc_u32 m0, m0, 0\n"
-            "v_writelane_b32 %[sw], %[w1], m0\n v_writelane_b32 %[sl], %[l1], m0\n v_writelane_b32 %[sh], %[h1], m0\n"
-            "s_cmp_lg_u64 %[m1], 0\n s_addc_u32 m0, m0, 0\n"
-            "v_writelane_b32 %[sw], %[w0], m0\n v_writelane_b32 %[sl], %[l0], m0\n v_writelane_b32 %[sh], %[h0], m0\n"
-            "s_cmp_lg_u64 %[m0], 0\n s_addc_u32 m0, m0, 0\n"
-            "s_sub_u32 m0, m0, 1\n"
-            "v_readlane_b32 %[cw], %[sw], m0\n v_readlane_b32 %[ml], %[sl], m0\n v_readlane_b32 %[mh], %[sh], m0\n"
-            "s_mov_b32 %[spn], m0"
-            : [spn] "=&s"(spn), [cw] "=&s"(cw), [ml] "=&s"(ml), [mh] "=&s"(mh), [sw] "+v"(stk_word),
-              [sl] "+v"(stk_mlo), [sh] "+v"(stk_mhi)
-            : [sp] "s"(sp), [w0] "s"(w[0]), [w1] "s"(w[1]), [w2] "s"(w[2]), [w3] "s"(w[3]), [m0] "s"(m[0]),
-              [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3]), [l0] "s"((uint32_t)m[0]), [l1] "s"((uint32_t)m[1]),
-              [l2] "s"((uint32_t)m[2]), [l3] "s"((uint32_t)m[3]), [h0] "s"((uint32_t)(m[0] >> 32)),
-              [h1] "s"((uint32_t)(m[1] >> 32)), [h2] "s"((uint32_t)(m[2] >> 32)), [h3] "s"((uint32_t)(m[3] >> 32))
-            : "m0", "scc");
-        // asm results count as divergent to the compiler: readfirstlane (folded away on
-        // SGPRs) tells it they are wave-uniform, so what follows stays on the scalar unit
-        spn = uniform(spn);
-        if (spn < floor) {  // nothing passed and nothing left above the floor
-            sp = floor;
-            mask = 0;
-            return;
-        }
-        sp = spn;
-        cur = (uint32_t)uniform((int)cw);
-        mask = ((unsigned long long)(uint32_t)uniform((int)mh) << 32 | (uint32_t)uniform((int)ml)) & ~done;
-        if (!mask) {
-            int n = 0;
-            if (!inner_pop(floor, done, n, mask, sp, stk_word, stk_mlo, stk_mhi)) return;
-            cur = (uint32_t)n;
-        }
-        if (cur & wide_leaf) return;
-    }
-#endif
     for (;;) {
         bool more;
 #ifdef YRT_WIDE_STATS
         nsteps++;
 #endif
         if (LDSN > 0 && cur < (uint32_t)(LDSN * wide_record_bytes)) {
-            float4 r[8];
+            float4 r[7];
             const float4* p = lds + (cur >> 4);
 #pragma unroll
-            for (int k = 0; k < 8; k++) r[k] = p[k];
+            for (int k = 0; k < 7; k++) r[k] = p[k];
             more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         } else {
-            float4 r[8];
+            float4 r[7];
             ld_wide_record(wbase, cur, r);
             more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         }
@@ -1400,16 +912,14 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     uint32_t cur = (uint32_t)S.wtop_root;
     unsigned long long mask = live;
     // the octant of the current level's rays when the whole wave shares it (8: mixed)
-    const int woct = YRT_WIDE_OCTANT ? wave_octant(wi, live) : 8;
+    const int woct = wave_octant(wi, live);
     int oct = woct;
-#if YRT_IDENT_INST
     // the instance-local direction of every instance whose rotation is the identity:
     // enter_direction on the identity frame is what entering any of them computes, bit for
     // bit (the same dot products, normalisation and reciprocals), so it is done once here
     vec3f icd, ici;
     enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
-    const int ioct = YRT_WIDE_OCTANT ? wave_octant(ici, live) : 8;
-#endif
+    const int ioct = wave_octant(ici, live);
     unsigned nsteps0 = 0, nsteps1 = 0;
 #ifdef YRT_WIDE_STATS
     unsigned ws[16] = {1, 0, 0, 0, 0, 0, 0, 0};
@@ -1422,7 +932,6 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                       base, 0);
 #define YRT_WD(o) wide_descend<o, LDSN>(S, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done, \
                                          level ? nsteps1 : nsteps0)
-#if YRT_WIDE_OCTANT
             switch (oct) {
                 case 0: YRT_WD(0); break;
                 case 1: YRT_WD(1); break;
@@ -1434,9 +943,6 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 case 7: YRT_WD(7); break;
                 default: YRT_WD(8); break;
             }
-#else
-            YRT_WD(8);
-#endif
 #undef YRT_WD
         }
         // ---- the leaf reached, if any ----
@@ -1458,7 +964,6 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 if (kind == kind_triangles) {
                     for (int i = first; i < first + count; i++) {
                         float t, w1, w2;
-#if YRT_APRIMS
                         // v0, e1, e2 as 9 packed dwords (yrt_device.h aprims): 9 SGPRs, not 12
                         const f4* abase = sgpr_ptr(reinterpret_cast<const f4*>(S.aprims));
                         sgpr8 a;
@@ -1470,18 +975,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                         const vec3f tv0 = {__int_as_float(a[0]), __int_as_float(a[1]), __int_as_float(a[2])};
                         const vec3f te1 = {__int_as_float(a[3]), __int_as_float(a[4]), __int_as_float(a[5])};
                         const vec3f te2 = {__int_as_float(a[6]), __int_as_float(a[7]), __int_as_float(b)};
-                        const bool h = tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, tv0, te1, te2, t, w1, w2, inl, mask);
-#else
-                        float4 pv[3];
-                        ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
-                        const bool h =
-                            tri_hit_nb<YRT_TRI_RCP>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, inl,
-                                                    mask);
-#endif
+                        const bool h = tri_hit_nb<true>(co, cd, tmin, tmax, tv0, te1, te2, t, w1, w2, inl, mask);
                         leaf_hit |= (h && inl) ? 1 : 0;
-                        // every lane of the leaf occluded: the leaf's other triangles cannot
-                        // change the answer
-                        if (YRT_LEAF_EARLY && !(mask & ~ballot(leaf_hit != 0))) break;
                     }
                 } else {
                     for (int i = first; i < first + count; i++) {
@@ -1507,41 +1002,30 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 if (inst_next < inst_end) {
                     const int k = inst_next++;
                     DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_end, sp, base, 0);
-                    constexpr int NR = YRT_WIDE_ROOTBOX ? winst_rows : 4;
-                    float4 fr[NR];
-                    ld_records_at<NR>(YRT_WIDE_ROOTBOX ? S.winst : S.tinst, (unsigned)(NR * k), fr);
+                    float4 fr[winst_rows];
+                    ld_records_at<winst_rows>(S.winst, (unsigned)(winst_rows * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
                     co = transform_point_inverse(f, wo);
-#if YRT_IDENT_INST
                     const bool ident = (uniform(ibits(fr[0].w)) & (int)inst_identity_bit) != 0;
                     if (ident)
                         cd = icd, ci = ici;
                     else
-#endif
                         enter_direction(f, wd, live & ~done, cd, ci);
                     const uint32_t rk = (uint32_t)uniform(ibits(fr[1].w));
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
                     mask = inst_mask & ~done;
-                    if constexpr (YRT_WIDE_ROOTBOX) {
+                    {
                         // the shape root's own box, which the wide root (its children's
                         // children) skips: the reference tests it first, and a lane that
                         // fails it finds nothing in this instance (every box below is
                         // inside it)
                         float tn;
-                        if constexpr (winst_rows == 5)
-                            mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[2].w, fr[3].w, fr[4].x, fr[4].y, fr[4].z,
-                                                    fr[4].w, tn));
-                        else
-                            mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[4].x, fr[4].y, fr[4].z, fr[NR - 1].x,
-                                                    fr[NR - 1].y, fr[NR - 1].z, tn));
+                        mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[2].w, fr[3].w, fr[4].x, fr[4].y, fr[4].z,
+                                                fr[4].w, tn));
                     }
                     WSTAT(3, 1u);
-#if YRT_IDENT_INST
-                    if (YRT_WIDE_OCTANT) oct = ident ? ioct : wave_octant(ci, live & ~done);
-#else
-                    if (YRT_WIDE_OCTANT) oct = wave_octant(ci, live & ~done);
-#endif
+                    oct = ident ? ioct : wave_octant(ci, live & ~done);
                     if (mask) break;
                     continue;
                 }

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_packet_kernel(dev_scene_vie
     work_counts wc;
     bool h;
     if (ANY)
-        h = S.wide ? packet_occluded_wide2(S, ray, valid) : packet_trace<true, false>(S, ray, valid, hr, wc);
+        h = S.wide ? packet_occluded_wide2(S, ray, valid) : packet_any<false>(S, ray, valid, wc);
     else
         h = packet_first<false>(S, ray, valid, hr, wc);
     if (valid) {

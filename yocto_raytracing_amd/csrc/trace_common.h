@@ -358,15 +358,6 @@ __device__ __forceinline__ bool occluded(const dev_scene_view& S, const ray3& wr
 // underflows f32), so the single rounding to f32 is the correctly rounded powf except
 // within ~2^-20 ulp of a rounding boundary -- the same exposure as a full f64 pow at a
 // fraction of its cost. pow(x, 0) = 1 for every x (log2(0) * 0 would be NaN).
-#ifndef YRT_POW_FULL
-#define YRT_POW_FULL 0
-#endif
-#ifndef YRT_POW_SHORTCUT
-#define YRT_POW_SHORTCUT 1  // the exact shortcuts of spec_pow / powf_cr below
-#endif
-#ifndef YRT_POW_CALL
-#define YRT_POW_CALL 1  // the f64 power path as a real call (its registers stay out of the callers' budget)
-#endif
 // the f64 path of powf_cr. Called, not inlined: the f64 log2/exp2 need ~40 VGPRs, which
 // inlined would count against the whole shading kernel's budget; as a call, the caller
 // spills what it has live around it, and only on the (rare) path that needs it.
@@ -374,27 +365,20 @@ __device__ __attribute__((noinline)) float pow_f64_path(float x, float y) {
     return (float)exp2((double)y * log2((double)x));
 }
 __device__ __forceinline__ float powf_cr(float x, float y) {
-#if YRT_POW_FULL
-    return (float)pow((double)x, (double)y);
-#else
     if (y == 0.0f) return 1.0f;
     // results below 2^-150 round to +0 (the f64 path gives exp2(-inf) = +0 for x = 0).
     // y * log2(x) < -151 by v_log_f32 (error ~2^-23 relative) puts the exact value below
     // -150 with a wide margin.
-    if (YRT_POW_SHORTCUT && y > 0.0f &&
-        (x == 0.0f || (x >= 0x1p-126f && x < 1.0f && y * __builtin_amdgcn_logf(x) < -151.0f)))
+    if (y > 0.0f && (x == 0.0f || (x >= 0x1p-126f && x < 1.0f && y * __builtin_amdgcn_logf(x) < -151.0f)))
         return 0.0f;
-    if (YRT_POW_CALL) return pow_f64_path(x, y);
-    return (float)exp2((double)y * log2((double)x));
-#endif
+    return pow_f64_path(x, y);
 }
 
 // the specular factor pow(x, y) as it multiplies ls = ks * (ke / r^2): when every
 // component of ls is +-0 (a material without Ks) and pow(x, y) is finite and >= +0
 // (x in [0, 1], y finite), ls * pow == ls * 1 bit for bit, and the pow is skipped.
 __device__ __forceinline__ float spec_pow(float x, float y, vec3f ls) {
-    if (YRT_POW_SHORTCUT && ls.x == 0.0f && ls.y == 0.0f && ls.z == 0.0f && x >= 0.0f && x <= 1.0f &&
-        y >= 0.0f && y <= flt_max)
+    if (ls.x == 0.0f && ls.y == 0.0f && ls.z == 0.0f && x >= 0.0f && x <= 1.0f && y >= 0.0f && y <= flt_max)
         return 1.0f;
     return powf_cr(x, y);
 }

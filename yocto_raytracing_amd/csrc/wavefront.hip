@@ -27,7 +27,6 @@
 #include <algorithm>
 #include <stdexcept>
 
-#include "packet_dual.h"
 #include "packet_trace.h"
 #include "trace_common.h"
 #include "yrt_render.h"
@@ -56,26 +55,12 @@ constexpr int shadow_block() { return PACKET ? YRT_SHADOW_BLOCK : WF_BLOCK; }
 #ifndef YRT_SHADOW_WAVES
 #define YRT_SHADOW_WAVES YRT_TRACE_WAVES  // the same for k_shadow
 #endif
-#ifndef YRT_EXP_SHADOW_LDS
-#define YRT_EXP_SHADOW_LDS 0  // experiment knob: dynamic LDS per shadow block (occupancy cap)
-#endif
-#ifndef YRT_PF2
-#define YRT_PF2 1  // closest hit: packet_first (goto-structured walk) instead of packet_trace<false>
-#endif
 #ifndef YRT_SHADOW_GRAB
-#define YRT_SHADOW_GRAB 8  // YRT_SHADOW_PERSIST 2: queue positions taken per atomic (A/B: 2 / 4 / 8 / 32: +82 / -0.8 / -1.9 / +2.4 %)
+#define YRT_SHADOW_GRAB 8  // k_shadow_persist: queue positions taken per atomic (A/B: 2 / 4 / 8 / 32: +82 / -0.8 / -1.9 / +2.4 %)
 #endif
 constexpr int MAX_LEVELS = 16;
-#ifndef YRT_CHUNK_LOG2
-#define YRT_CHUNK_LOG2 29  // samples per chunk, non-reflective scenes (~70 B of HBM each)
-#endif
-#ifndef YRT_LEVEL_PRUNE
-#define YRT_LEVEL_PRUNE 1  // reflective scenes: stop launching levels once one spawns no ray
-#endif
-#ifndef YRT_TILE
-#define YRT_TILE 8
-#endif
-constexpr int TILE = YRT_TILE;  // pixel tiles of TILE x TILE in the sample enumeration
+constexpr int CHUNK_LOG2 = 29;  // samples per chunk, non-reflective scenes (~70 B of HBM each)
+constexpr int TILE = 8;         // pixel tiles of TILE x TILE in the sample enumeration
 
 struct wf_buffers {
     f4* surf0;          // {p.xyz, info}: info = mat*4+kind, -1 miss, -2 not a sample
@@ -86,12 +71,11 @@ struct wf_buffers {
     // bounce levels (reflective scenes only)
     f4* ray_o[MAX_LEVELS];  // level k >= 1: {o.xyz, parent index}
     f4* ray_d[MAX_LEVELS];  // level k >= 1: {d.xyz, -}
-    f4* R[MAX_LEVELS];      // level k >= 1 radiance (level 0 uses rad)
     f4* rec0[MAX_LEVELS];   // level k: {D.xyz, child index}
     f4* rec1[MAX_LEVELS];   // {la.xyz, -}
     f4* rec2[MAX_LEVELS];   // {kr.xyz, -}
     int* count;             // count[k]: rays at level k (k >= 1)
-    unsigned* queue;        // per-XCD work counters of the persistent kernels: [0, 8) shadow, [8, 16) primary
+    unsigned* queue;        // per-XCD work counters of the persistent shadow kernel: [0, 8)
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
 };
@@ -118,11 +102,7 @@ __device__ __forceinline__ bool pixel_of(const dev_render_args& A, int tiles_x, 
     return i < A.width && j < A.height;
 }
 
-template <bool COUNT>
 __device__ __forceinline__ void flush(unsigned long long* counters, int idx, unsigned long long v) {
-#ifdef YRT_EXP_NOCOUNT  // diagnostic: no per-wave counter atomics in the timed kernels
-    if (!COUNT) return;
-#endif
     unsigned long long s = wave_sum(v);
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(counter_line(counters) + idx, s);
 }
@@ -151,13 +131,13 @@ __device__ __forceinline__ void flush_block(unsigned long long* counters, const 
 }
 
 __device__ __forceinline__ void flush_work(unsigned long long* counters, const work_counts& wc) {
-    flush<true>(counters, cnt_box_tests, wc.box);
-    flush<true>(counters, cnt_inst_entries, wc.inst);
-    flush<true>(counters, cnt_prim_tests, wc.prim);
-    flush<true>(counters, cnt_shaded_hits, wc.hits);
-    flush<true>(counters, cnt_tex_lookups, wc.tex);
-    flush<true>(counters, cnt_wave_node_visits, wc.wnode);
-    flush<true>(counters, cnt_wave_prim_visits, wc.wprim);
+    flush(counters, cnt_box_tests, wc.box);
+    flush(counters, cnt_inst_entries, wc.inst);
+    flush(counters, cnt_prim_tests, wc.prim);
+    flush(counters, cnt_shaded_hits, wc.hits);
+    flush(counters, cnt_tex_lookups, wc.tex);
+    flush(counters, cnt_wave_node_visits, wc.wnode);
+    flush(counters, cnt_wave_prim_visits, wc.wprim);
 }
 
 __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool hit, const surface& sf) {
@@ -179,10 +159,10 @@ struct tracer {
     __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
                                           work_counts& wc) {
         if (PACKET) {
-#if YRT_PF2
-            if constexpr (!ANY) return packet_first<COUNT>(S, ray, valid, hr, wc);
-#endif
-            return packet_trace<ANY, COUNT>(S, ray, valid, hr, wc);
+            if constexpr (ANY)
+                return packet_any<COUNT>(S, ray, valid, wc);
+            else
+                return packet_first<COUNT>(S, ray, valid, hr, wc);
         }
         if (!valid) return false;
         if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
@@ -213,21 +193,13 @@ __device__ __forceinline__ tracer<ANY, COUNT, PACKET, SE> make_tracer(traversal_
     return t;
 }
 
-#ifndef YRT_XCD_REMAP
-#define YRT_XCD_REMAP 0  // 1: contiguous tile ranges per XCD (A/B at c4: primary +10 %, shadow +7.5 % -- the
-                         // regions differ in cost, and the slowest XCD sets the launch time)
-#endif
 // Workgroups are dealt round-robin to the 8 XCDs (linear block b runs on XCD b % 8).
-// Remap so that each XCD's blocks take one contiguous range of the grid: neighbouring
-// tiles trace neighbouring rays through the same BVH nodes, so each XCD's L2 (and each
-// CU's scalar cache) sees one region of the image instead of every eighth tile of all
-// of it. A bijection for any grid size.
-#ifndef YRT_XCD_CHUNK
-#define YRT_XCD_CHUNK 64  // YRT_XCD_REMAP 2: blocks per XCD run
-#endif
-// YRT_XCD_REMAP 2 keeps the round-robin sweep over the image but hands each XCD runs of
-// YRT_XCD_CHUNK consecutive blocks: the grid is cut into super-chunks of 8 runs, XCD x
-// takes run x of each (a bijection; a ragged last super-chunk keeps its blocks).
+// xcd_runs keeps the round-robin sweep over the image but hands each XCD runs of C
+// consecutive blocks: the grid is cut into super-chunks of 8 runs, XCD x takes run x of
+// each (a bijection; a ragged last super-chunk keeps its blocks). Each XCD then traces
+// neighbouring pixels (its L2 and its CUs' scalar caches see one region) while all eight
+// still sweep the image together. (Contiguous block ranges per XCD lose: +10 % primary,
+// +7.5 % shadow -- image regions differ in cost and the slowest XCD sets the launch time.)
 template <unsigned C>
 __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
     constexpr unsigned G = 8u * C;
@@ -237,23 +209,11 @@ __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
 }
 
 #ifndef YRT_SHADOW_LIGHT_MINOR
-#define YRT_SHADOW_LIGHT_MINOR 24  // k_shadow: XCD run length with the light index minor (0: light-major round robin; A/B: shadow -1.1 %)
+#define YRT_SHADOW_LIGHT_MINOR 24  // k_shadow: XCD run length with the light index minor (A/B: shadow -1.1 %)
 #endif
 #ifndef YRT_XCD_CHUNK_PRIMARY
-#define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (0: plain round robin)
+#define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (A/B: -1.5 %)
 #endif
-
-__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
-#if YRT_XCD_REMAP == 2
-    return xcd_runs<YRT_XCD_CHUNK>(b, n);
-#elif YRT_XCD_REMAP
-    const unsigned x = b % 8u, j = b / 8u, q = n / 8u, r = n % 8u;
-    return x * q + (x < r ? x : r) + j;
-#else
-    (void)n;
-    return b;
-#endif
-}
 
 // ---- level 0: camera rays + closest hit + surface ----
 // the camera samples idx of one wave: eval_camera, closest hit, surface record
@@ -281,12 +241,7 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     if (valid) {
         surface sf = {};
         if (hit) {
-#ifdef YRT_EXP_NOSURF  // timing diagnostic only (the image is wrong): the walk without the surface
-            sf.p = {hr.dist, hr.ew.y, hr.ew.z};
-            sf.mat = hr.slot & 3;
-#else
             sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
-#endif
             if (COUNT) wc.hits++;
         }
         store_surface(B, idx, hit, sf);
@@ -301,86 +256,11 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
     constexpr int BS = YRT_PRIMARY_BLOCK;
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
-#if YRT_XCD_CHUNK_PRIMARY && !YRT_XCD_REMAP
     const int idx = (int)xcd_runs<YRT_XCD_CHUNK_PRIMARY>(blockIdx.x, gridDim.x) * BS + threadIdx.x;
-#else
-    const int idx = (int)xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
-#endif
     work_counts wc;
     const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, idx, wc);
     flush_block<2, BS>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
     if (COUNT) flush_work(counters, wc);
-}
-
-// the same, persistent (YRT_PRIMARY_PERSIST): a resident grid whose waves take the
-// 64-sample blocks from one queue per XCD, YRT_SHADOW_GRAB at a time, in XCD runs of
-// YRT_XCD_CHUNK_PRIMARY blocks (k_shadow_persist's scheme)
-#ifndef YRT_PRIMARY_PERSIST
-#define YRT_PRIMARY_PERSIST 0  // A/B at c4: primary +9 % (runs of 256 or 64 blocks alike)
-#endif
-#ifndef YRT_PRIMARY_STRIDE
-#define YRT_PRIMARY_STRIDE 1  // YRT_PRIMARY_PERSIST: a batch's positions one row of waves apart
-#endif
-constexpr int PP_BLOCK = packet_block;  // packet_first parks 1/d per thread in LDS: <= packet_block threads
-template <bool COUNT, bool PACKET, typename SE>
-__global__ __launch_bounds__(PP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(dev_scene_view S, dev_render_args A,
-                                                                              chunk_args C, wf_buffers B, int nblocks,
-                                                                              unsigned long long* counters) {
-    constexpr int WPB = PP_BLOCK / 64;
-    constexpr unsigned RUN = YRT_XCD_CHUNK_PRIMARY > 0 ? YRT_XCD_CHUNK_PRIMARY : 1;
-    constexpr unsigned G = YRT_SHADOW_GRAB;
-    __shared__ traversal_lds<PACKET, SE> lds;
-    auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
-    const unsigned lane = threadIdx.x & 63;
-    const unsigned xcd = blockIdx.x % 8u;
-    const unsigned n = (unsigned)nblocks;
-    const unsigned full = n / (8u * RUN) * (8u * RUN), per_xcd = full / 8u;
-    auto issue = [&]() -> unsigned {
-        unsigned v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add(B.queue + 8 + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return v;
-    };
-    unsigned qv = issue(), qb = 0, qleft = 0;
-    unsigned nvalid = 0;  // wave-uniform
-    work_counts wc;
-    auto block_of = [&](unsigned q) {
-        return q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
-    };
-#if YRT_PRIMARY_STRIDE
-    // batch k = the G positions (k / W) * W*G + k % W + j*W, j < G (W = the XCD's waves):
-    // waves move through the positions in rows of W together, so the XCD's active window
-    // stays ~W positions wide instead of W*G (each wave's G items come W apart)
-    const unsigned W = gridDim.x / 8u * (PP_BLOCK / 64u);
-    unsigned qk = 0;
-    for (;;) {
-        if (qleft == 0) {
-            qk = (unsigned)__builtin_amdgcn_readfirstlane((int)qv);
-            qleft = G;
-            qv = issue();
-            if (block_of((qk / W) * (W * G) + qk % W) >= n) break;  // positions grow with the batch
-        }
-        const unsigned q = (qk / W) * (W * G) + qk % W + (G - qleft) * W;
-        qleft--;
-        const unsigned b = block_of(q);
-        if (b >= n) continue;
-#else
-    for (;;) {
-        if (qleft == 0) {
-            qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
-            qleft = G;
-            qv = issue();
-        }
-        const unsigned q = qb++;
-        qleft--;
-        const unsigned b = block_of(q);
-        if (b >= n) break;
-#endif
-        const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, (int)(b * 64u + lane), wc);
-        nvalid += (unsigned)__popcll(ballot(valid));
-    }
-    (void)WPB;
-    const unsigned long long mine = lane == 0 ? (unsigned long long)nvalid : 0ull;
-    flush_block<2, PP_BLOCK>(counters, {cnt_rays, cnt_samples}, {mine, mine});
 }
 
 // ---- levels >= 1: closest hit of the compacted mirror rays (grid-stride) ----
@@ -431,18 +311,12 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     const int n = level ? B.count[level] : nsamp_level0;
     // level 0 (one block per 256 samples and light): the remap runs over the whole
     // (x, light) grid; levels >= 1 are grid-stride and keep their blocks
-#if YRT_SHADOW_LIGHT_MINOR
     // a pixel block's lights in neighbouring blocks (light index minor), dealt in XCD runs
     const unsigned lin = level ? blockIdx.x
                                : xcd_runs<YRT_SHADOW_LIGHT_MINOR>(blockIdx.y * gridDim.x + blockIdx.x,
                                                                   gridDim.x * gridDim.y);
     const int li = level ? (int)blockIdx.y : (int)(lin % gridDim.y);
     const int bx = level ? (int)blockIdx.x : (int)(lin / gridDim.y);
-#else
-    const unsigned lin = level ? blockIdx.x : xcd_block(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-    const int li = level ? (int)blockIdx.y : (int)(lin / gridDim.x);
-    const int bx = level ? (int)blockIdx.x : (int)(lin % gridDim.x);
-#endif
     const f4* lr = S.lights + 6 * li;
     const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
     const vec3f lp0 = xyz(ld4(lr + 4));
@@ -478,15 +352,15 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     flush_block<1, BS>(counters, {cnt_shadow_rays}, {rays});
     if (COUNT) {
         flush_work(counters, wc);
-        flush<true>(counters, cnt_shadow_box_tests, wc.box);
-        flush<true>(counters, cnt_shadow_inst_entries, wc.inst);
-        flush<true>(counters, cnt_shadow_prim_tests, wc.prim);
-        flush<true>(counters, cnt_shadow_wave_node_visits, wc.wnode);
+        flush(counters, cnt_shadow_box_tests, wc.box);
+        flush(counters, cnt_shadow_inst_entries, wc.inst);
+        flush(counters, cnt_shadow_prim_tests, wc.prim);
+        flush(counters, cnt_shadow_wave_node_visits, wc.wnode);
     }
 }
 
 // ---- shadow rays of level 0, persistent: a grid of SP_BLOCK-thread blocks that fills the
-// chip once (YRT_SHADOW_PERSIST); every wave walks its own share of the (64-sample
+// chip once; every wave walks its own share of the (64-sample
 // block, light) items, so no block launch, block retirement or per-block counter flush
 // happens per item. LDSN > 0: each block first stages the first LDSN 4-wide records --
 // the breadth-first top of the instance tree (device_scene.cpp emit_bfs) -- in LDS, and
@@ -498,9 +372,6 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 // consecutive items (k_shadow's XCD runs), its waves interleaved over them, so all eight
 // XCDs sweep the image together while each traces neighbouring pixels. Items past the
 // last whole super-run are dealt round-robin to every wave.
-#ifndef YRT_SHADOW_PERSIST
-#define YRT_SHADOW_PERSIST 2  // 0: one block per item; 1: fixed interleave (A/B +21 %); 2: per-XCD queue (A/B -1.9 %)
-#endif
 #ifndef YRT_SHADOW_PERSIST_MIN_ITEMS
 // the persistent grid pays a tail (its waves' last batches, ~0.26 ms) that the hardware's
 // block dealing does not, and saves the dealing's per-block cost (~6 % of the walk time
@@ -509,23 +380,17 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 // 0.8 M (rank 0 of 8) +13 %)
 #define YRT_SHADOW_PERSIST_MIN_ITEMS 2000000
 #endif
-#ifndef YRT_SHADOW_PERSIST_LEVELS
-#define YRT_SHADOW_PERSIST_LEVELS 0  // the persistent shadow kernel for the mirror levels too (A/B at c3: shadow +32 %)
-#endif
 #ifndef YRT_SHADOW_LDS_RECORDS
 #define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
 #endif
-#ifndef YRT_SP_BLOCK
-#define YRT_SP_BLOCK 1024  // threads per persistent shadow block (two blocks per CU at 8 waves/SIMD)
-#endif
-constexpr int SP_BLOCK = YRT_SP_BLOCK;
+constexpr int SP_BLOCK = 1024;  // threads per persistent shadow block (two blocks per CU at 8 waves/SIMD)
 
 template <int LDSN>
 __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(dev_scene_view S, int nsamp,
                                                                                 int nx, wf_buffers B,
                                                                                 unsigned long long* counters) {
     constexpr int WPB = SP_BLOCK / 64;  // waves per block
-    constexpr unsigned C = YRT_SHADOW_LIGHT_MINOR > 0 ? YRT_SHADOW_LIGHT_MINOR : 24;
+    constexpr unsigned C = YRT_SHADOW_LIGHT_MINOR;
     __shared__ float4 lds_nodes[LDSN > 0 ? LDSN * 8 : 1];
     if constexpr (LDSN > 0) {
         const int nrec = LDSN * 8;
@@ -543,18 +408,14 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     const unsigned n_items = (unsigned)nx * (unsigned)nl;
     const unsigned wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
-    const unsigned waves_xcd = (gridDim.x / 8u) * WPB;       // gridDim.x is a multiple of 8
-    const unsigned j = (blockIdx.x / 8u) * WPB + wv;          // this wave's index on its XCD
-    const unsigned total_waves = gridDim.x * WPB;
-    const unsigned gw = blockIdx.x * WPB + wv;
+    (void)wv;
     const unsigned full = n_items / (8u * C) * (8u * C);     // items in whole super-runs
     const unsigned per_xcd = full / 8u;
     unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays traced by this wave
-    // YRT_SHADOW_PERSIST 2: the waves of an XCD take the positions of its item sequence
-    // from one agent-scope counter (one atomic per item, issued an item ahead), which
-    // keeps the chip's working window as tight as the hardware's block dealing does;
-    // 1: a fixed interleave (wave j takes j, j + waves_xcd, ...)
-    // the atomic's result stays in lane 0's VGPR until the next item needs it: it is
+    // the waves of an XCD take the positions of its item sequence from one agent-scope
+    // counter (one atomic per batch, issued a batch ahead), which keeps the chip's working
+    // window as tight as the hardware's block dealing does (a fixed interleave, wave j
+    // taking j, j + W, ..., lets the waves drift apart: +21 %); the atomic's result stays in lane 0's VGPR until the next item needs it: it is
     // issued after this item's surface load and before its walk (the walk reads only
     // through the scalar cache), so its latency hides behind the walk
     auto issue = [&]() -> unsigned {
@@ -566,25 +427,18 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     // ~11 M atomics/s per address; taking single positions near the end of the sequence
     // contends there and loses, A/B: full frame +1.5 %, an eighth of it +11 %)
     constexpr unsigned G = YRT_SHADOW_GRAB;
-    unsigned qv = YRT_SHADOW_PERSIST == 2 ? issue() : 0u;  // next batch, lane 0
-    unsigned qb = 0, qleft = 0;                            // current batch (uniform)
-    unsigned qj = j;
+    unsigned qv = issue();           // next batch, lane 0
+    unsigned qb = 0, qleft = 0;      // current batch (uniform)
     // q: this wave's position in its XCD's item sequence; every bound is wave-uniform,
     // so the whole wave reaches every walk
     for (;;) {
-        unsigned q;
-        if (YRT_SHADOW_PERSIST == 2) {
-            if (qleft == 0) {
-                qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
-                qleft = G;
-                qv = issue();
-            }
-            qleft--;
-            q = qb++;
-        } else {
-            q = qj;
-            qj += waves_xcd;
+        if (qleft == 0) {
+            qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
+            qleft = G;
+            qv = issue();
         }
+        qleft--;
+        const unsigned q = qb++;
         // runs of C items per XCD, then the tail items past the last whole super-run
         const unsigned it = q < per_xcd ? ((q / C) * 8u + xcd) * C + q % C : full + (q - per_xcd) * 8u + xcd;
         if (it >= n_items) break;
@@ -611,110 +465,14 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         const bool occ = packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
     }
-    (void)gw;
-    (void)total_waves;
     const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
     flush_block<1, SP_BLOCK>(counters, {cnt_shadow_rays}, {mine});
-}
-
-// ---- shadow rays of level 0, two rays per lane (YRT_SHADOW_DUAL): lane l traces sample l
-// of two neighbouring pixels to the same light (packet_dual.h), so the wave-uniform walk
-// is shared by 128 rays. Persistent, with k_shadow_persist's per-XCD queues; an item is
-// (pixel pair, light), light index minor.
-#ifndef YRT_SHADOW_DUAL
-#define YRT_SHADOW_DUAL 0  // A/B at c4: shadow +9 % at 6 waves/SIMD, +12.5 % at 5 (SALU -17 %, VALU +4 %, SMEM -31 %)
-#endif
-#ifndef YRT_SHADOW_DUAL_WAVES
-#define YRT_SHADOW_DUAL_WAVES 6  // register budget of the two-ray walk (waves per SIMD)
-#endif
-constexpr int SD_BLOCK = 256;
-
-__device__ __forceinline__ bool shadow_ray_of(const wf_buffers& B, const frame3f& lf, vec3f lp0, int idx, int nsamp,
-                                              ray3& sr) {
-    sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
-    if (idx >= nsamp) return false;
-    const float4 s0 = ld4(B.surf0 + idx);
-    if (ibits(s0.w) < 0) return false;
-    const vec3f p = xyz(s0);
-    const vec3f tp = transform_point(lf, lp0 - p);
-    const vec3f l = normalize(tp);
-    const float r = length(tp);
-    sr = {p, l, 0.01f, r - 0.01f};  // raytrace.cpp:128-133
-    return true;
-}
-
-__global__ __launch_bounds__(SD_BLOCK, YRT_SHADOW_DUAL_WAVES) void k_shadow_dual(dev_scene_view S, int nsamp, int nx,
-                                                                                  wf_buffers B,
-                                                                                  unsigned long long* counters) {
-    constexpr unsigned C = YRT_SHADOW_LIGHT_MINOR > 0 ? YRT_SHADOW_LIGHT_MINOR : 24;
-    constexpr unsigned G = YRT_SHADOW_GRAB;
-    const int nl = S.nlights;
-    const unsigned npairs = (unsigned)(nx + 1) / 2u;
-    const unsigned n_items = npairs * (unsigned)nl;
-    const unsigned lane = threadIdx.x & 63;
-    const unsigned xcd = blockIdx.x % 8u;
-    const unsigned full = n_items / (8u * C) * (8u * C), per_xcd = full / 8u;
-    auto issue = [&]() -> unsigned {
-        unsigned v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return v;
-    };
-    unsigned qv = issue(), qb = 0, qleft = 0;
-    unsigned rays = 0;  // wave-uniform
-    for (;;) {
-        if (qleft == 0) {
-            qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
-            qleft = G;
-            qv = issue();
-        }
-        const unsigned q = qb++;
-        qleft--;
-        const unsigned it = q < per_xcd ? ((q / C) * 8u + xcd) * C + q % C : full + (q - per_xcd) * 8u + xcd;
-        if (it >= n_items) break;
-        const int li = (int)(it % (unsigned)nl);
-        const int bp = (int)(it / (unsigned)nl);
-        const f4* lr = S.lights + 6 * li;
-        const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
-        const vec3f lp0 = xyz(ld4(lr + 4));
-        const int ia = (2 * bp) * 64 + (int)lane, ib = ia + 64;
-        ray3 ra, rb;
-        const bool va = shadow_ray_of(B, lf, lp0, ia, nsamp, ra);
-        const bool vb = shadow_ray_of(B, lf, lp0, ib, nsamp, rb);
-        rays += (unsigned)__popcll(ballot(va)) + (unsigned)__popcll(ballot(vb));
-        bool oa, ob;
-        packet_occluded_dual(S, ra, va, rb, vb, oa, ob);
-        if (va) B.occl[(size_t)li * B.capacity + ia] = oa ? 1 : 0;
-        if (vb) B.occl[(size_t)li * B.capacity + ib] = ob ? 1 : 0;
-    }
-    const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
-    flush_block<1, SD_BLOCK>(counters, {cnt_shadow_rays}, {mine});
 }
 
 // ---- shade() after the queries (raytrace.cpp:99-206) ----
 // FUSE (level 0 of a scene without mirrors, s*s dividing the block): the block's
 // samples are whole pixels, so the ordered per-pixel sum of k_accumulate is done here
 // from LDS and the per-sample radiance never goes to HBM.
-#ifndef YRT_SHADE_FUSE64
-#define YRT_SHADE_FUSE64 0  // 1: fused k_shade in one-wave blocks when a pixel fits (A/B: +9 %)
-#endif
-#ifndef YRT_SHADE_SMAT
-#define YRT_SHADE_SMAT 0  // k_shade: a wave-uniform material record through the scalar cache (A/B: c4 shade +12 %)
-#endif
-#ifndef YRT_EAGER_FOLD
-#define YRT_EAGER_FOLD 1  // reflective scenes: k_shade folds final values up the mirror chain (no k_fold_children)
-#endif
-#ifndef YRT_SHADE_SLIGHT
-#define YRT_SHADE_SLIGHT 1  // k_shade: light records through the scalar cache
-#endif
-#ifndef YRT_SHADE_OCC4
-#define YRT_SHADE_OCC4 1  // k_shade: occlusion bytes of <= 4 lights loaded with the surface
-#endif
-#ifndef YRT_SHADE_POW_FIRST
-#define YRT_SHADE_POW_FIRST 0  // k_shade: the specular powers in a pass of their own (A/B: c4 shade +22 %, c3 -5 %; VGPRs 95 natural)
-#endif
-#ifndef YRT_SHADE_SUM3
-#define YRT_SHADE_SUM3 1  // fused k_shade: the per-pixel sums one lane per colour component
-#endif
 #ifndef YRT_SHADE_WAVES
 #define YRT_SHADE_WAVES 7  // k_shade register budget: 65-73 VGPRs with the f64 pow called (A/B at c4: 5 -> 7 waves -4 %; with the pow inlined it needed 96)
 #endif
@@ -725,8 +483,6 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
     const int n = level ? B.count[level] : nsamp_level0;
-    constexpr bool POWF = YRT_SHADE_POW_FIRST && OCC4;
-    __shared__ float spow_lds[POWF ? 4 : 1][POWF ? SB : 1];
     __shared__ float4 fused_rad[FUSE ? SB : 1];
     __shared__ int cmp_count[SB / 64], cmp_base[SB / 64];
     work_counts wc;
@@ -762,16 +518,6 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 const int mat = info >> 2, kind = info & 3;
                 const vec3f ro = level ? xyz(ld4(B.ray_o[level] + idx)) : cam_o;
                 float4 m0, m1, m2, m3;
-#if YRT_SHADE_SMAT
-                // a wave on one material (the usual case: a pixel's samples) reads its
-                // record through the scalar cache, one 64 B load
-                const int mat_w = __builtin_amdgcn_readfirstlane(mat);
-                if (__ballot(mat != mat_w) == 0) {
-                    float4 mr[4];
-                    ld_scalar_at<4>(S.mats, (unsigned)(4 * mat_w), mr);
-                    m0 = mr[0], m1 = mr[1], m2 = mr[2], m3 = mr[3];
-                } else
-#endif
                 {
                     m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1);
                     m2 = ld4(S.mats + 4 * mat + 2), m3 = ld4(S.mats + 4 * mat + 3);
@@ -790,56 +536,15 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 vec3f c = {0.0f, 0.0f, 0.0f};
                 // raytrace.cpp:147 (per light) and :196 (mirror): the same value each time
                 const vec3f v = normalize(ro - p);
-#if YRT_SHADE_POW_FIRST
-                if constexpr (OCC4) {
-                    // the specular powers first, each in a loop iteration of its own, with
-                    // only what they need live: the f64 exp2/log2 path (rare: most calls
-                    // take spec_pow's exact shortcuts) no longer adds its ~40 VGPRs to the
-                    // full shading state, and the kernel fits 8 waves per SIMD. The inputs
-                    // are the same float operations as in the loop below, so the values
-                    // are the same.
-                    for (int li = 0; li < S.nlights; li++) {
-                        float sp = 1.0f;
-                        if (((occ_bits >> li) & 1u) == 0u) {
-                            float4 lrec[6];
-                            ld_scalar<6>(S.lights + 6 * li, lrec);
-                            const frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
-                            const vec3f lp0 = xyz(lrec[4]), ke = xyz(lrec[5]);
-                            const vec3f tp = transform_point(lf, lp0 - p);
-                            const vec3f l = normalize(tp);
-                            const float r = length(tp);
-                            const vec3f h = normalize(v + l);
-                            vec3f ks = ks0;
-                            if (ks_txt >= 0) ks = ks * tks;
-                            const vec3f ls = ks * (ke / (r * r));
-                            float x;
-                            if (kind == kind_lines) {
-                                float prodnh = dot(nrm, h);
-                                if (prodnh < 0.0f) prodnh *= -1;
-                                x = __builtin_sqrtf(1.0f - prodnh);
-                            } else {
-                                x = smax(0.0f, dot(nrm, h));
-                            }
-                            sp = spec_pow(x, ns, ls);
-                        }
-                        spow_lds[li][threadIdx.x] = sp;
-                    }
-                }
-#endif
                 for (int li = 0; li < S.nlights; li++) {
                     if (OCC4 ? ((occ_bits >> li) & 1u) != 0u : B.occl[(size_t)li * B.capacity + idx] != 0) continue;
                     const f4* lr = S.lights + 6 * li;
-#if YRT_SHADE_SLIGHT
                     // the light record is the same for every lane (li is the loop index):
                     // one scalar fetch instead of six 64-lane vector loads of one address
                     float4 lrec[6];
                     ld_scalar<6>(lr, lrec);
                     frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
                     vec3f lp0 = xyz(lrec[4]), ke = xyz(lrec[5]);
-#else
-                    frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
-                    vec3f lp0 = xyz(ld4(lr + 4)), ke = xyz(ld4(lr + 5));
-#endif
                     vec3f tp = transform_point(lf, lp0 - p);
                     vec3f l = normalize(tp);
                     float r = length(tp);
@@ -857,10 +562,10 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                         float sinnl = __builtin_sqrtf(1.0f - prodnl);
                         float sinnh = __builtin_sqrtf(1.0f - prodnh);
                         ld = ld * sinnl;
-                        ls = ls * (POWF ? spow_lds[li][threadIdx.x] : spec_pow(sinnh, ns, ls));
+                        ls = ls * spec_pow(sinnh, ns, ls);
                     } else {
                         ld = ld * smax(0.0f, dot(nrm, l));
-                        ls = ls * (POWF ? spow_lds[li][threadIdx.x] : spec_pow(smax(0.0f, dot(nrm, h)), ns, ls));
+                        ls = ls * spec_pow(smax(0.0f, dot(nrm, h)), ns, ls);
                     }
                     c = c + (ld + ls);
                 }
@@ -884,7 +589,6 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
             if (FUSE) {
                 fused_rad[threadIdx.x] = make_float4(R.x, R.y, R.z, 1.0f);
             } else if (write_r) {
-#if YRT_EAGER_FOLD
                 // a final value at level k >= 1 folds straight up its chain of parents
                 // (raytrace.cpp:201-206, R_k-1 = (D + R_k * kr) + la, in that order) to
                 // the camera sample; each parent has this one child, so its value is
@@ -901,10 +605,6 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                     col = cc, node = parent, lev--;
                 }
                 B.rad[node] = {col.x, col.y, col.z, 1.0f};
-#else
-                f4* dst = level ? B.R[level] : B.rad;
-                dst[idx] = {R.x, R.y, R.z, 1.0f};
-#endif
             }
         }
         // compaction of the mirror rays: one atomic per BLOCK (a shared counter hit by
@@ -936,9 +636,9 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
         // raytrace.cpp:232-249: s*s samples of a pixel summed in jj/ii order, then / s*s
         __syncthreads();
         const int ppb = SB / C.spp;
-#if YRT_SHADE_SUM3
-        // one lane per (pixel, colour component): each lane's sum is the same ordered chain
-        // of adds as the float4 loop below, with a third of the dependent adds per lane
+        // one lane per (pixel, colour component): each lane's sum is the reference's ordered
+        // chain of adds (raytrace.cpp:232-249) for that component, so a pixel's three
+        // dependent chains run side by side (A/B: c4 shade 2.00 -> 1.96 ms)
         for (int t = (int)threadIdx.x; t < 3 * ppb; t += SB) {
             const int px = t / 3, comp = t - 3 * px;
             const int pl = (int)(blockIdx.x * SB / C.spp) + px;
@@ -957,48 +657,9 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 if (comp == 0) o[3] = valid ? 1.0f : 0.0f;
             }
         }
-#else
-        if ((int)threadIdx.x < ppb) {
-            const int pl = (int)(blockIdx.x * SB / C.spp) + threadIdx.x;
-            int lx, ly, i, j;
-            const bool valid = pl < C.npix && pixel_of(A, C.tiles_x, C.pix0 + pl, lx, ly, i, j);
-            if (pl < C.npix && lx < A.tile_w && ly < A.tile_h) {
-                float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (valid) {
-                    vec4f acc = {0, 0, 0, 0};
-                    const float4* r = fused_rad + threadIdx.x * C.spp;
-                    for (int q = 0; q < C.spp; q++) {
-                        const float4 c = r[q];
-                        acc = {acc.x + c.x, acc.y + c.y, acc.z + c.z, acc.w + 1.0f};
-                    }
-                    const float d = float(C.spp);
-                    o = make_float4(acc.x / d, acc.y / d, acc.z / d, 1.0f);
-                }
-                out[(size_t)ly * A.out_stride + lx] = o;
-            }
-        }
-#endif
     }
-    flush<false>(counters, cnt_depth_truncated, truncated);
+    flush(counters, cnt_depth_truncated, truncated);
     if (COUNT) flush_work(counters, wc);
-}
-
-// ---- fold level k+1 back onto its mirror samples at level k (raytrace.cpp:201-206):
-// R_k = (D_k + R_{k+1}*kr_k) + la_k, one lane per child ray (its parent is ray_o.w) ----
-__global__ __launch_bounds__(WF_BLOCK) void k_fold_children(int level, wf_buffers B) {
-    // one lane per CHILD ray at level+1: its parent sample is ray_o.w
-    const int n = B.count[level + 1];
-    f4* dst_base = level ? B.R[level] : B.rad;
-    for (int c = blockIdx.x * WF_BLOCK + threadIdx.x; c < n; c += gridDim.x * WF_BLOCK) {
-        const int parent = ibits(B.ray_o[level + 1][c].w);
-        float4 r = ld4(B.R[level + 1] + c);
-        float4 d = ld4(B.rec0[level] + parent), la = ld4(B.rec1[level] + parent), kr = ld4(B.rec2[level] + parent);
-        vec3f col = {r.x, r.y, r.z};
-        vec3f cc = {d.x, d.y, d.z};
-        cc = cc + vec3f{col.x * kr.x, col.y * kr.y, col.z * kr.z};
-        cc = cc + xyz(la);
-        dst_base[parent] = {cc.x, cc.y, cc.z, 1.0f};
-    }
 }
 
 // ---- ordered per-pixel sum (raytrace.cpp:232-249) ----
@@ -1046,9 +707,8 @@ size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
     size_t b = align_up(sizeof(int) * (MAX_LEVELS + 1)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
-    // levels >= 1: ray_o, ray_d (+ R without the eager fold); levels < last: rec0..2
-    if (nlevels > 1)
-        b += (size_t)(nlevels - 1) * (YRT_EAGER_FOLD ? 2 : 3) * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
+    // levels >= 1: ray_o, ray_d; levels < last: rec0..2
+    if (nlevels > 1) b += (size_t)(nlevels - 1) * 2 * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
     return b;
 }
 
@@ -1071,7 +731,6 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
     for (int k = 1; k < nlevels; k++) {
         B.ray_o[k] = (f4*)take(16 * c);
         B.ray_d[k] = (f4*)take(16 * c);
-        B.R[k] = YRT_EAGER_FOLD ? nullptr : (f4*)take(16 * c);
     }
     for (int k = 0; k + 1 < nlevels; k++) {
         B.rec0[k] = (f4*)take(16 * c);
@@ -1094,7 +753,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     // samples per chunk: a whole frame at c3/c4, 15 chunks at c5. A reflective scene keeps
     // per-level buffers for every level (~100 B per sample and level). The chunk is
     // halved until the workspace takes at most half of the free HBM.
-    long long target = ds.reflective ? (1ll << 25) : (1ll << YRT_CHUNK_LOG2);
+    long long target = ds.reflective ? (1ll << 25) : (1ll << CHUNK_LOG2);
     auto cap_for = [&](long long tgt) {
         int pix = (int)std::max<long long>(1, std::min<long long>(npix_total, tgt / spp));
         pix = ((pix + TILE * TILE - 1) / (TILE * TILE)) * TILE * TILE;
@@ -1123,14 +782,9 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
     phase_timer& T = ds.timer;
     const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
-    // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE)
-#ifndef YRT_NO_FUSE
-    // fused shade blocks of one wave when a pixel's samples fit (s <= 8), else of WF_BLOCK
-    const int fuse_block = (YRT_SHADE_FUSE64 && 64 % spp == 0) ? 64 : WF_BLOCK;
-    const bool fuse = nlevels == 1 && fuse_block % spp == 0;
-#else
-    const bool fuse = false;
-#endif
+    // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE;
+    // one-wave fused blocks lose: +9 %)
+    const bool fuse = nlevels == 1 && WF_BLOCK % spp == 0;
     for (long long pix0 = 0; pix0 < npix_total; pix0 += pix_per_chunk) {
         chunk_args C = {pix0, (int)std::min<long long>(pix_per_chunk, npix_total - pix0), spp, tiles_x};
         const int nsamp = C.npix * spp;
@@ -1142,32 +796,19 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         int t = T.begin(phase_primary, stream);
         constexpr int TB = shadow_block<PACKET>();
         const int tgrid = (nsamp + TB - 1) / TB;
-        if (YRT_PRIMARY_PERSIST && !COUNT && PACKET) {
-            hipError_t e = hipMemsetAsync(B.queue + 8, 0, 8 * sizeof(unsigned), stream);
-            if (e != hipSuccess) return e;
-            const int nb = ds.num_cus * (YRT_TRACE_WAVES * 4 * 64 / PP_BLOCK);
-            hipLaunchKernelGGL((k_primary_persist<COUNT, PACKET, SE>), dim3(nb), dim3(PP_BLOCK), 0, stream, ds.view,
-                               A, C, B, (nsamp + 63) / 64, counters);
-        } else {
-            hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>),
-                               dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK), dim3(YRT_PRIMARY_BLOCK), 0,
-                               stream, ds.view, A, C, B, counters);
-        }
+        hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
+                           dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
         T.end(t, stream);
         // levels run: a level with no mirror rays ends the chunk's recursion (the host reads
         // the next level's ray count once per level; the per-level launches it saves cost
         // more than the read)
-        int levels_run = nlevels;
         for (int level = 0; level < nlevels; level++) {
-            if (level > 0 && YRT_LEVEL_PRUNE) {
+            if (level > 0) {
                 int cnt = 0;
                 hipError_t e = hipMemcpyAsync(&cnt, B.count + level, sizeof(int), hipMemcpyDeviceToHost, stream);
                 if (e == hipSuccess) e = hipStreamSynchronize(stream);
                 if (e != hipSuccess) return e;
-                if (cnt == 0) {
-                    levels_run = level;
-                    break;
-                }
+                if (cnt == 0) break;
             }
             if (level > 0) {
                 t = T.begin(phase_bounce, stream);
@@ -1178,18 +819,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
-                if (YRT_SHADOW_DUAL && !COUNT && PACKET && ds.wide_ok && level == 0 && TB == 64) {
-                    hipError_t e = hipMemsetAsync(B.queue, 0, 8 * sizeof(unsigned), stream);
-                    if (e != hipSuccess) return e;
-                    const int nb = ds.num_cus * (YRT_SHADOW_DUAL_WAVES * 4 * 64 / SD_BLOCK);
-                    hipLaunchKernelGGL(k_shadow_dual, dim3(nb), dim3(SD_BLOCK), 0, stream, ds.view, nsamp, tgrid, B,
-                                       counters);
-                } else if (YRT_SHADOW_PERSIST && !COUNT && PACKET && ds.wide_ok && TB == 64 &&
-                           (level == 0 || YRT_SHADOW_PERSIST_LEVELS) &&
-                           (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS) {
+                if (!COUNT && PACKET && ds.wide_ok && TB == 64 && level == 0 &&
+                    (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS) {
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
-                    if (YRT_SHADOW_PERSIST == 2) {
+                    {
                         hipError_t e = hipMemsetAsync(B.queue, 0, 8 * sizeof(unsigned), stream);
                         if (e != hipSuccess) return e;
                     }
@@ -1201,15 +835,15 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                         hipLaunchKernelGGL((k_shadow_persist<0>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
                                            level ? -level - 1 : nsamp, tgrid, B, counters);
                 } else if (!COUNT && PACKET && ds.wide_ok)
-                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), YRT_EXP_SHADOW_LDS,
+                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), 0,
                                        stream, ds.view, level, nsamp, B, counters);
                 else
-                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, false>), sg, dim3(TB), YRT_EXP_SHADOW_LDS,
+                    hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, false>), sg, dim3(TB), 0,
                                        stream, ds.view, level, nsamp, B, counters);
                 T.end(t, stream);
             }
             t = T.begin(phase_shade, stream);
-            const bool occ4 = YRT_SHADE_OCC4 && ds.nlights <= 4;
+            const bool occ4 = ds.nlights <= 4;
 #define YRT_SHADE_LAUNCH(FU, SBV, GRID)                                                                          \
     do {                                                                                                        \
         if (occ4)                                                                                               \
@@ -1220,19 +854,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                nsamp, A.max_depth, B, counters, C, out);                                        \
     } while (0)
             if (fuse) {
-                if (fuse_block == 64)
-                    YRT_SHADE_LAUNCH(true, 64, dim3((nsamp + 63) / 64));
-                else
-                    YRT_SHADE_LAUNCH(true, WF_BLOCK, dim3(grid));
+                YRT_SHADE_LAUNCH(true, WF_BLOCK, dim3(grid));
             } else {
                 YRT_SHADE_LAUNCH(false, WF_BLOCK, dim3(level ? stride_grid : grid));
             }
 #undef YRT_SHADE_LAUNCH
-            T.end(t, stream);
-        }
-        for (int level = YRT_EAGER_FOLD ? -1 : levels_run - 2; level >= 0; level--) {
-            t = T.begin(phase_fold, stream);
-            hipLaunchKernelGGL(k_fold_children, dim3(stride_grid), dim3(WF_BLOCK), 0, stream, level, B);
             T.end(t, stream);
         }
         if (!fuse) {

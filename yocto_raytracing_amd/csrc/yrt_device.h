@@ -22,10 +22,9 @@
 //   wnodes  8 x f4 per 4-wide node of the any-hit walk (device_scene.cpp wide_builder):
 //           {lo.x[4]} {lo.y[4]} {lo.z[4]} {hi.x[4]} {hi.y[4]} {hi.z[4]} {ref[4]} {info[4]},
 //           instance level and all shapes in one array, absolute indices
-//   winst   6 x f4 per instance-BVH leaf slot for the any-hit walk: tinst's four rows, then
-//           the object-space root box of the instance's shape {lo, -} {hi, -} (the box the
-//           reference tests first on entering it, scene.cpp:386-442); five rows with
-//           YRT_WINST5 (see winst_rows)
+//   winst   5 x f4 per instance-BVH leaf slot for the any-hit walk: the frame and the
+//           object-space root box of the instance's shape (the box the reference tests
+//           first on entering it, scene.cpp:386-442), packed as winst_rows describes
 //   aprims  9 floats per sprims slot: a triangle's v0, e1, e2 packed (the any-hit leaf loads)
 #pragma once
 
@@ -51,14 +50,11 @@ constexpr uint32_t leaf_bit = 0x80000000u;
 constexpr uint32_t inst_identity_bit = 0x40000000u;
 constexpr uint32_t inst_shape_mask = 0x3fffffffu;
 
-// winst (the any-hit walk's instance records): YRT_WINST5 packs what that walk reads into
-// five rows -- {frame.x, tinst row 0 .w} {frame.y, wide root | kind} {frame.z, box lo.x}
+// winst (the any-hit walk's instance records) packs what that walk reads into five rows --
+// {frame.x, tinst row 0 .w} {frame.y, wide root | kind} {frame.z, box lo.x}
 // {frame.o, box lo.y} {box lo.z, hi.x, hi.y, hi.z} -- one s_load_dwordx16 + x4 (20 SGPRs)
 // instead of tinst's four rows plus two box rows (x16 + x8, 24 SGPRs)
-#ifndef YRT_WINST5
-#define YRT_WINST5 1
-#endif
-constexpr int winst_rows = YRT_WINST5 ? 5 : 6;
+constexpr int winst_rows = 5;
 
 // 4-wide any-hit records (device_scene.cpp wide_builder): 128 bytes per wide node --
 // six f4 rows of child bounds {lo.x[4]}, {lo.y[4]}, {lo.z[4]}, {hi.x[4]}, {hi.y[4]},
@@ -69,19 +65,10 @@ constexpr uint32_t wide_leaf = 0x80000000u;
 constexpr int wide_count_shift = 28;
 constexpr uint32_t wide_index_mask = 0x0fffffffu;
 constexpr int wide_record_bytes = 128;
-#ifndef YRT_SPINE
-#define YRT_SPINE 2
-#endif
-constexpr int spine_len = YRT_SPINE;  // nodes per closest-hit walk record (2..4)
+constexpr int spine_len = 2;  // nodes per closest-hit walk record (a node and its child start+1)
 // spine records (tpair/spair): spine_len x {lo, hi} f4 pairs; an inner node's lo.w is
 // the byte offset of its child start's record (child start+1's is the next record)
-// YRT_FIRST_FILTER: each closest-hit record also carries the boxes of X's child start
-// (L) and of R's child start (RL), so the walk can drop, at push time, the lanes whose
-// later reference test of L / RL must fail (a box test is monotone in tmax); 128 bytes
-#ifndef YRT_FIRST_FILTER
-#define YRT_FIRST_FILTER 0  // A/B at c4: primary +5.4 % (13.43 -> 14.15 ms), identical image
-#endif
-constexpr int spine_record_bytes = YRT_FIRST_FILTER ? 128 : 32 * spine_len;
+constexpr int spine_record_bytes = 32 * spine_len;
 constexpr int spine_record_f4 = spine_record_bytes / 16;
 
 struct dev_scene_view {
