@@ -9,6 +9,7 @@
 //   raytrace          src/raytrace.cpp:213
 //   eval_camera/shade src/raytrace.cpp:6,88 (row-subset render, same loop body as :228-250)
 //   intersect_first/any src/scene.cpp:483,489
+//   save_hdr_or_ldr   src/image.cpp:81   (stbi_write_hdr / tonemap + stbi_write_png)
 // and to serialise the reference's in-memory scene / BVH into the repo's own
 // interchange formats (.yrtscene, .yrtbvh; spec in DESIGN.md §3) so the product
 // loader and BVH builder can be compared byte-for-byte with the reference.
@@ -341,6 +342,15 @@ int ref_load_image4b(const char* path, int* w, int* h, unsigned char* out) {
     *h = img.height;
     if (out) memcpy(out, img.pixels.data(), img.pixels.size() * 4);
     return img.pixels.empty() ? -1 : 0;
+}
+
+// The reference's own image writer (image.cpp:81-88 save_hdr_or_ldr: stbi_write_hdr for
+// .hdr, tonemap + stbi_write_png otherwise) on a caller-supplied RGBA float frame.
+int ref_save_image(const char* path, const float* rgba, int w, int h) {
+    image4f img(w, h);
+    memcpy(img.pixels.data(), rgba, (size_t)w * h * 16);
+    save_hdr_or_ldr(path, img);
+    return 0;
 }
 
 }  // extern "C"

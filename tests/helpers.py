@@ -157,6 +157,49 @@ def read_png_rgba8(path) -> np.ndarray:
     return raw[:, 1:].reshape(h, w, 4)
 
 
+def decode_png_rgba8(data: bytes) -> np.ndarray:
+    """Decode an 8-bit RGBA, non-interlaced PNG with any of the five row filters
+    (stbi_write_png picks one per row, yrt_save_image writes filter 0)."""
+    import struct
+    import zlib
+
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n = struct.unpack(">I", data[pos:pos + 4])[0]
+        typ = data[pos + 4:pos + 8]
+        if typ == b"IHDR":
+            w, h, depth, ctype, _, _, interlace = struct.unpack(">IIBBBBB", data[pos + 8:pos + 21])
+            assert (depth, ctype, interlace) == (8, 6, 0), "only RGBA8, non-interlaced"
+        elif typ == b"IDAT":
+            idat += data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, w * 4 + 1)
+    out = np.zeros((h, w * 4), np.int32)
+    for y in range(h):
+        f, cur = raw[y, 0], raw[y, 1:].astype(np.int32)
+        up = out[y - 1] if y else np.zeros(w * 4, np.int32)
+        if f in (0, 2):
+            out[y] = (cur + (up if f == 2 else 0)) & 255
+            continue
+        row = np.zeros(w * 4, np.int32)
+        for x in range(w * 4):
+            a = row[x - 4] if x >= 4 else 0
+            b = up[x]
+            c = up[x - 4] if x >= 4 else 0
+            if f == 1:
+                pred = a
+            elif f == 3:
+                pred = (a + b) // 2
+            else:  # Paeth
+                p = a + b - c
+                pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
+                pred = a if pa <= pb and pa <= pc else (b if pb <= pc else c)
+            row[x] = (cur[x] + pred) & 255
+        out[y] = row
+    return out.astype(np.uint8).reshape(h, w, 4)
+
+
 def assert_same_floats(got, want):
     """bit-for-bit equality, except that a NaN only has to be a NaN: its sign and
     payload follow the GPU's NaN propagation, not x86's"""

@@ -321,7 +321,8 @@ def raytrace(scn, amb: Sequence[float] = (0.1, 0.1, 0.1), resolution: int = 720,
         try:
             p = render_params(amb, resolution, samples, width=width, max_depth=max_depth, camera=camera,
                               count_work=count_work, algorithm=algorithm)
-            W, H = scn.upload(devices[0]).image_size(p)
+            W, H = scn.image_size(resolution, camera)  # host-side: no extra replica on devices[0]
+            W = int(width) or W
             img = np.zeros((H, W, 4), np.float32)
             ms.render_into(p, img.ctypes.data)
             stats = ms.last_stats()

@@ -596,10 +596,16 @@ int yrt_save_image_mem(const char* path, const float* rgba, int w, int h, int me
         const size_t n = (size_t)w * h;
         hipStream_t st = (hipStream_t)stream;
         if (p.size() >= 4 && p.substr(p.size() - 4) == ".hdr") {
-            std::vector<float> px(n * 4);
-            hip_check(hipMemcpyAsync(px.data(), rgba, n * 16, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
-            hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-            yrt::save_hdr_or_ldr(p, px.data(), w, h);
+            // RGBE on the GPU (4 B/pixel over PCIe), the run-length scanlines on the host
+            unsigned char* d8 = nullptr;
+            hip_check(hipMalloc(&d8, n * 4), "hipMalloc(rgbe)");
+            std::vector<unsigned char> rgbe(n * 4);
+            hipError_t e = yrt::launch_rgbe(rgba, w, h, d8, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(rgbe.data(), d8, n * 4, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            (void)hipFree(d8);
+            hip_check(e, "device rgbe");
+            yrt::save_hdr_rgbe(p, rgbe.data(), w, h);
             return YRT_OK;
         }
         // tonemap on the GPU, then only the 8-bit image crosses PCIe

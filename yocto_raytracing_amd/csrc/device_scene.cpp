@@ -326,6 +326,21 @@ device_scene* device_scene_create(const scene& scn, int device) {
     for (auto& s : scn.shapes)
         if (!binary(s.bvh)) throw unsupported_error("shape BVH of " + s.name + " is not binary (unsupported)");
 
+    // the walks address records with 32-bit offsets (the s_load SGPR offset is an unsigned
+    // 32-bit byte offset; the packed any-hit triangles' offset is a signed int): 48 B per
+    // primitive slot (sprims), 36 B (aprims), 64 B / 80 B per instance slot (tinst / winst)
+    {
+        uint64_t nslots = 0;
+        for (auto& s : scn.shapes) nslots += s.bvh.leaf_prims.size();
+        const uint64_t ninst = scn.bvh.leaf_prims.size();
+        if (nslots * 48 >= (1ull << 32) || nslots * 36 >= (1ull << 31))
+            throw unsupported_error("scene too large: " + std::to_string(nslots) +
+                                    " primitive slots exceed the walks' 32-bit record offsets");
+        if (ninst * 16 * (uint64_t)std::max(4, winst_rows) >= (1ull << 32))
+            throw unsupported_error("scene too large: " + std::to_string(ninst) +
+                                    " instances exceed the walks' 32-bit record offsets");
+    }
+
     auto ds = new device_scene();
     ds->device = device;
     ds->cameras = scn.cameras;

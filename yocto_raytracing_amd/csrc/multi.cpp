@@ -336,6 +336,14 @@ int yrt_multi_render(yrt_multi* m, const yrt_render_params* p, float* out, int m
             for (int r = 0; r < n; r++) th.emplace_back(render_rank, r);
             for (auto& t : th) t.join();
         }
+        if (std::any_of(status.begin(), status.end(), [](int st) { return st != YRT_OK; })) {
+            // the other ranks' streams may still run kernels that write their shards: let
+            // them drain before the error leaves (a later grow() or yrt_multi_free would
+            // otherwise free buffers in use); their own errors are ignored here
+            for (int r = 0; r < n; r++)
+                if (hipSetDevice(m->devices[r]) == hipSuccess) (void)hipStreamSynchronize(m->streams[r]);
+            (void)hipGetLastError();
+        }
         for (int r = 0; r < n; r++)
             if (status[r] != YRT_OK) {
                 yrt::set_last_error(msg[r].c_str());

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "packet_trace.h"
+#include "rgbe.h"
 #include "trace_common.h"
 #include "yrt_render.h"
 
@@ -253,7 +254,34 @@ __global__ void tonemap_kernel(const float4* __restrict__ in, int n, uchar4* __r
                          (unsigned char)(sclamp(h.w, 0.0f, 1.0f) * 255));
 }
 
+// the .hdr writer's RGBE bytes (rgbe.h, stbiw__linear_to_rgbe), one lane per pixel, in
+// the layout save_hdr_rgbe consumes: per row four component planes for run-length
+// encoded widths (neighbouring lanes write neighbouring bytes of a plane), else
+// interleaved quadruples. Only these 4 B/pixel cross PCIe instead of the 16 B floats.
+__global__ void rgbe_kernel(const float4* __restrict__ in, int w, int h, unsigned char* __restrict__ out) {
+    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= (long long)w * h) return;
+    const float4 p = in[k];
+    unsigned char e[4];
+    linear_to_rgbe(p.x, p.y, p.z, e);
+    if (rgbe_rle_width(w)) {
+        const long long j = k / w, i = k - j * w;
+        unsigned char* row = out + j * 4 * w + i;
+        row[0] = e[0], row[w] = e[1], row[2 * (long long)w] = e[2], row[3 * (long long)w] = e[3];
+    } else {
+        reinterpret_cast<uchar4*>(out)[k] = make_uchar4(e[0], e[1], e[2], e[3]);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_rgbe(const float* rgba, int w, int h, unsigned char* out, hipStream_t stream) {
+    if (w <= 0 || h <= 0) return hipSuccess;
+    const long long n = (long long)w * h;
+    hipLaunchKernelGGL(rgbe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float4*)rgba, w,
+                       h, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_render(device_scene& ds, const dev_render_args& args, void* out_rgba,
                          unsigned long long* counters, bool count_work, hipStream_t stream) {

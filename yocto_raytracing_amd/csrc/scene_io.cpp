@@ -10,10 +10,12 @@
 // Image output restates tonemap + save_hdr_or_ldr (src/image.cpp:55-88).
 #include <zlib.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
 
+#include "rgbe.h"
 #include "yrt_scene.h"
 
 namespace yrt {
@@ -233,39 +235,90 @@ void tonemap_thresholds(float thr[256]) {
     }
 }
 
-void save_hdr_or_ldr(const std::string& filename, const float* px, int w, int h) {
+// RGBE bytes of a frame in the layout the scanline writer consumes: for run-length
+// encoded widths each row as four planes (all R bytes, all G, all B, all E: the
+// per-component runs of stbiw__write_hdr_scanline), otherwise interleaved quadruples.
+// The device encoder (render.hip launch_rgbe) produces the same bytes.
+void rgbe_encode(const float* px, int w, int h, unsigned char* out) {
+    const bool planar = rgbe_rle_width(w);
+    for (int j = 0; j < h; j++)
+        for (int i = 0; i < w; i++) {
+            const float* p = px + ((size_t)j * w + i) * 4;
+            unsigned char e[4];
+            linear_to_rgbe(p[0], p[1], p[2], e);
+            for (int c = 0; c < 4; c++)
+                out[planar ? ((size_t)j * 4 + c) * w + i : ((size_t)j * w + i) * 4 + c] = e[c];
+        }
+}
+
+namespace {
+// one component plane of a scanline, run-length encoded as the reference's writer does
+// (stb_image_write.h:562-612): literal stretches in records of <= 128 bytes (a count
+// byte, then the bytes) up to the next run of >= 3 equal bytes, that run in records of
+// <= 127 (128 + count, then the byte), repeated to the end of the plane
+void rle_plane(const unsigned char* v, int w, std::vector<unsigned char>& out) {
+    int x = 0;
+    while (x < w) {
+        int run = x;  // first position of a run of three, if one starts before w - 2
+        while (run + 2 < w && !(v[run] == v[run + 1] && v[run] == v[run + 2])) run++;
+        const bool has_run = run + 2 < w;
+        const int lit_end = has_run ? run : w;
+        while (x < lit_end) {
+            const int n = std::min(lit_end - x, 128);
+            out.push_back((unsigned char)n);
+            out.insert(out.end(), v + x, v + x + n);
+            x += n;
+        }
+        if (has_run) {
+            int end = run;
+            while (end < w && v[end] == v[run]) end++;
+            while (x < end) {
+                const int n = std::min(end - x, 127);
+                out.push_back((unsigned char)(128 + n));
+                out.push_back(v[x]);
+                x += n;
+            }
+        }
+    }
+}
+}  // namespace
+
+// stbi_write_hdr (stb_image_write.h:617-637): its header lines, then per row either the
+// flat quadruples or {2, 2, w >> 8, w & 255} and the four run-length encoded planes
+void save_hdr_rgbe(const std::string& filename, const unsigned char* rgbe, int w, int h) {
+    std::vector<unsigned char> buf;
+    const std::string head = "#?RADIANCE\n# Written by stb_image_write.h\nFORMAT=32-bit_rle_rgbe\n"
+                             "EXPOSURE=          1.0000000000000\n\n-Y " +
+                             std::to_string(h) + " +X " + std::to_string(w) + "\n";
+    buf.insert(buf.end(), head.begin(), head.end());
+    const size_t row = (size_t)w * 4;
+    if (!rgbe_rle_width(w)) {
+        buf.insert(buf.end(), rgbe, rgbe + row * h);
+    } else {
+        for (int j = 0; j < h; j++) {
+            const unsigned char hdr[4] = {2, 2, (unsigned char)((w & 0xff00) >> 8), (unsigned char)(w & 0xff)};
+            buf.insert(buf.end(), hdr, hdr + 4);
+            for (int c = 0; c < 4; c++) rle_plane(rgbe + (size_t)j * row + (size_t)c * w, w, buf);
+        }
+    }
     FILE* f = fopen(filename.c_str(), "wb");
     if (!f) throw std::runtime_error("cannot write " + filename);
-    bool hdr = filename.size() >= 4 && filename.substr(filename.size() - 4) == ".hdr";
+    const size_t wrote = fwrite(buf.data(), 1, buf.size(), f);
+    const int closed = fclose(f);
+    if (wrote != buf.size() || closed != 0) throw std::runtime_error("cannot write " + filename);
+}
+
+void save_hdr_or_ldr(const std::string& filename, const float* px, int w, int h) {
+    const bool hdr = filename.size() >= 4 && filename.substr(filename.size() - 4) == ".hdr";
     if (hdr) {
-        // Radiance RGBE, flat (uncompressed) scanlines
-        fprintf(f, "#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y %d +X %d\n", h, w);
-        std::vector<unsigned char> row((size_t)w * 4);
-        for (int j = 0; j < h; j++) {
-            for (int i = 0; i < w; i++) {
-                const float* p = px + ((size_t)j * w + i) * 4;
-                float m = std::fmax(p[0], std::fmax(p[1], p[2]));
-                unsigned char* e = &row[(size_t)i * 4];
-                if (!(m >= 1e-32f)) {
-                    e[0] = e[1] = e[2] = e[3] = 0;
-                } else {
-                    int ex;
-                    float n = std::frexp(m, &ex) * 256.0f / m;
-                    e[0] = (unsigned char)(p[0] * n);
-                    e[1] = (unsigned char)(p[1] * n);
-                    e[2] = (unsigned char)(p[2] * n);
-                    e[3] = (unsigned char)(ex + 128);
-                }
-            }
-            fwrite(row.data(), 1, row.size(), f);
-        }
+        std::vector<unsigned char> rgbe((size_t)w * h * 4);
+        rgbe_encode(px, w, h, rgbe.data());
+        save_hdr_rgbe(filename, rgbe.data(), w, h);
     } else {
-        std::vector<unsigned char> ldr((size_t)w * h * 4), png;
+        std::vector<unsigned char> ldr((size_t)w * h * 4);
         tonemap_rgba8(px, w, h, ldr.data());
-        png_encode_rgba8(ldr.data(), w, h, png);
-        fwrite(png.data(), 1, png.size(), f);
+        save_ldr_png(filename, ldr.data(), w, h);
     }
-    fclose(f);
 }
 
 void save_ldr_png(const std::string& filename, const unsigned char* rgba8, int w, int h) {

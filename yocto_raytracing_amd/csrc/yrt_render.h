@@ -85,6 +85,8 @@ struct tonemap_table {
 };
 hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, const tonemap_table& table,
                           hipStream_t stream);
+// the .hdr writer's RGBE bytes on the device (rgbe.h; the layout of rgbe_encode)
+hipError_t launch_rgbe(const float* rgba, int w, int h, unsigned char* out, hipStream_t stream);
 
 // traversal stack entries per lane (LDS resident): instance level + shape level
 constexpr int traversal_stack_cap = 40;

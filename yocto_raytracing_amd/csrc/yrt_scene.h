@@ -143,5 +143,10 @@ int tonemap_neg_inf_level();  // the level of -inf (pow(-inf, 1/2.2) = +inf)
 void save_hdr_or_ldr(const std::string& filename, const float* rgba, int w, int h);
 // PNG of an already tonemapped RGBA8 image (the device-tonemap path of yrt_save_image_mem)
 void save_ldr_png(const std::string& filename, const unsigned char* rgba8, int w, int h);
+// the .hdr writer in two halves: RGBE bytes of a frame (rows as four component planes when
+// the width is run-length encoded, else interleaved; rgbe.h), then the reference's file
+// (stbi_write_hdr's header and scanlines). The device path encodes on the GPU.
+void rgbe_encode(const float* rgba, int w, int h, unsigned char* out);
+void save_hdr_rgbe(const std::string& filename, const unsigned char* rgbe, int w, int h);
 
 }  // namespace yrt
