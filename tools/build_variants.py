@@ -7,6 +7,8 @@ writes yocto_raytracing_amd/variants/libyrt_<name>.so (git-ignored, travels to t
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -21,6 +23,7 @@ def main(argv):
     b.build_library()
     out_dir = PKG / "variants"
     out_dir.mkdir(exist_ok=True)
+    jobs, libs = [], []
     for spec in argv:
         name, _, defs = spec.partition(":")
         defines = [d for d in defs.split(",") if d]
@@ -33,9 +36,18 @@ def main(argv):
                 cmd = [b.HIPCC, *b.COMMON, *b.DEVICE_FLAGS, *defines, f"--offload-arch={b.ARCH}", "-c", str(b.CSRC / src), "-o", str(o)]
             else:
                 cmd = [b.CLANGXX, *b.COMMON, *b.HOST_DEFS, *defines, "-c", str(b.CSRC / src), "-o", str(o)]
-            subprocess.run(cmd, check=True, capture_output=True)
+            jobs.append(cmd)
             objs.append(o)
-        lib = out_dir / f"libyrt_{name}.so"
+        libs.append((out_dir / f"libyrt_{name}.so", objs))
+
+    def run(cmd):
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError(" ".join(map(str, cmd)) + "\n" + r.stderr[-4000:])
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        list(ex.map(run, jobs))
+    for lib, objs in libs:
         subprocess.run([b.HIPCC, "-shared", "-fPIC", f"--offload-arch={b.ARCH}", "-o", str(lib), *map(str, objs), *b.LINK_LIBS],
                        check=True)
         print(lib)
