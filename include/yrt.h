@@ -48,7 +48,9 @@ typedef struct yrt_render_params {
     int resolution;    /* vertical resolution -r (raytrace.cpp:216) */
     int width;         /* 0: round(camera.aspect * resolution) as the reference; >0: explicit */
     int samples;       /* -s: samples PER AXIS, s*s per pixel (raytrace.cpp:232-234) */
-    int max_depth;     /* trace_first calls per camera sample; reference: unbounded. 0 -> 16 */
+    int max_depth;     /* trace_first calls per camera sample; reference: unbounded. 0 -> 16.
+                          Any depth with the wavefront algorithms (per-level records in HBM);
+                          the megakernel keeps 16 per lane (deeper: YRT_ERR_UNSUPPORTED) */
     int camera;        /* camera index; reference: cameras.front() == 0 */
     int x0, y0;        /* window origin in image pixels */
     int tile_w, tile_h;/* window size; 0 -> to the image edge */

@@ -88,6 +88,11 @@ typedef struct {
     shape* shps;
     instance* ists;
     bvh tree;
+    /* the instances shade()'s light loop acts on (material ke > 0 in every component), in
+     * instance order: the loop over all instances skips the others without effect, so
+     * visiting only these is the same computation (raytrace.cpp:121-125) */
+    int nlight;
+    int* light;
 } scene;
 
 /* ---------------- vmath.h ---------------- */
@@ -452,11 +457,9 @@ static v3 shade(const scene* s, v3 amb, const ray* r, int depth, ctx* cx) {
     const texture* tks = m->ks_txt >= 0 ? &s->texs[m->ks_txt] : 0;
     v3 la = mul(amb, m->kd);
     if (tkd) la = mul(la, eval_tex(tkd, uv));
-    for (int li = 0; li < s->nist; li++) {
-        const instance* L = &s->ists[li];
-        if (L->mat < 0) continue;
+    for (int lk = 0; lk < s->nlight; lk++) {
+        const instance* L = &s->ists[s->light[lk]];
         v3 ke = s->mats[L->mat].ke;
-        if (!(ke.x > 0.0f && ke.y > 0.0f && ke.z > 0.0f)) continue;
         v3 lpos = s->shps[L->shp].pos[0];
         v3 l = normalize(xform_point(&L->f, sub(lpos, p)));
         float rr = length(xform_point(&L->f, sub(lpos, p)));
@@ -574,6 +577,13 @@ void* oracle_load(const char* path) {
     s->ists = (instance*)calloc(n ? n : 1, sizeof(instance));
     for (uint32_t i = 0; ok && i < n; i++) ok = rd(f, &s->ists[i], sizeof(instance));
     gzclose(f);
+    s->light = (int*)calloc(n ? n : 1, sizeof(int));
+    for (uint32_t i = 0; ok && i < n; i++) {
+        const instance* L = &s->ists[i];
+        if (L->mat < 0 || L->mat >= s->nmat) continue;
+        const v3 ke = s->mats[L->mat].ke;
+        if (ke.x > 0.0f && ke.y > 0.0f && ke.z > 0.0f) s->light[s->nlight++] = (int)i;
+    }
     if (!ok || build_scene_bvh(s) < 0) {
         oracle_free(s);
         return 0;
@@ -590,7 +600,7 @@ void oracle_free(void* vs) {
         free(sh->pos); free(sh->norm); free(sh->tc); free(sh->rad); free(sh->pts); free(sh->lines);
         free(sh->tris); free(sh->tree.nodes); free(sh->tree.leaf);
     }
-    free(s->cams); free(s->texs); free(s->mats); free(s->shps); free(s->ists);
+    free(s->cams); free(s->texs); free(s->mats); free(s->shps); free(s->ists); free(s->light);
     free(s->tree.nodes); free(s->tree.leaf);
     free(s);
 }

@@ -163,5 +163,101 @@ def main():
     print("lines", dig["lines"], "hit fraction", hit.mean(), "any", ahit.mean())
 
 
+MIRROR_RENDERS = [(48, 1), (36, 2)]
+MIRROR_DEPTH = 64  # the GPU's max_depth for these fixtures (the reference has no cap)
+
+
+def build_mirrors(path: Path):
+    """A mirror corridor: two parallel mirror walls 2 apart along x in [0, 100], a
+    diffuse floor, two point lights, and a camera between the walls turned 30 degrees
+    toward one of them, so that camera rays bounce between the walls ~20-36 times before
+    they leave the corridor (past the reference-free 16-level cap of round 2)."""
+    import yocto_raytracing_amd as yrt
+
+    s = yrt.Scene.create()
+    th = np.deg2rad(30.0)
+    d = np.array([np.cos(th), 0.0, np.sin(th)], np.float32)
+    z = -d
+    x = np.cross([0, 1, 0], z).astype(np.float32)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x).astype(np.float32)
+    eye = np.array([0.5, 0.0, 0.0], np.float32)
+    s.add_camera(np.concatenate([x, y, z, eye]), fovy=0.12, aspect=16 / 9, focus=10.0)
+    m_mirror = s.add_material(kd=(0.05, 0.06, 0.07), ks=(0.2, 0.2, 0.2), kr=(0.85, 0.8, 0.75), rs=0.3)
+    m_mirror2 = s.add_material(kd=(0.07, 0.05, 0.04), ks=(0.1, 0.1, 0.1), kr=(0.8, 0.85, 0.9), rs=0.25)
+    m_floor = s.add_material(kd=(0.4, 0.35, 0.3), ks=(0.05, 0.05, 0.05), rs=0.5)
+    m_light = s.add_material(ke=(40, 38, 36))
+    m_light2 = s.add_material(ke=(20, 25, 30))
+
+    def wall(zc, nz, ny=8, nx=50):
+        xs = np.linspace(0, 100, nx + 1, dtype=np.float32)
+        ys = np.linspace(-4, 4, ny + 1, dtype=np.float32)
+        gx, gy = np.meshgrid(xs, ys)
+        pos = np.stack([gx.ravel(), gy.ravel(), np.full(gx.size, zc, np.float32)], 1)
+        tris = []
+        for j in range(ny):
+            for i in range(nx):
+                a, b, c, e = j * (nx + 1) + i, j * (nx + 1) + i + 1, (j + 1) * (nx + 1) + i + 1, (j + 1) * (nx + 1) + i
+                tris += [(a, b, c), (a, c, e)] if nz > 0 else [(a, c, b), (a, e, c)]
+        return s.add_shape(pos, norm=np.tile([0, 0, nz], (len(pos), 1)), texcoord=pos[:, :2] / 10,
+                           triangles=np.array(tris))
+
+    w0 = wall(-1.0, 1.0)
+    w1 = wall(1.0, -1.0)
+    fp = np.array([[0, -4, -1], [100, -4, -1], [100, -4, 1], [0, -4, 1]], np.float32)
+    floor = s.add_shape(fp, norm=np.tile([0, 1, 0], (4, 1)), texcoord=fp[:, [0, 2]], triangles=[[0, 2, 1], [0, 3, 2]])
+    light = s.add_shape([[0, 0, 0]], norm=[[0, 0, 1]], texcoord=[[0, 0]], radius=[0.001], points=[0])
+    s.add_instance(frame(), w0, m_mirror)
+    s.add_instance(frame(), w1, m_mirror2)
+    s.add_instance(frame(), floor, m_floor)
+    s.add_instance(frame(o=(30, 3, 0)), light, m_light)
+    s.add_instance(frame(o=(70, 3, 0.5)), light, m_light2)
+    s.save(str(path))
+    return s
+
+
+def make_mirrors():
+    """scenes/mirrors.yrtscene + the reference's renders (unbounded recursion) and rays"""
+    import ctypes as C
+
+    from make_golden import load_ref, sample_rays, trace
+
+    spath = HERE / "scenes" / "mirrors.yrtscene"
+    build_mirrors(spath)
+    lib = load_ref()
+    lib.ref_read_scene.restype = lib.ref_load_scene.restype
+    lib.ref_read_scene.argtypes = lib.ref_load_scene.argtypes
+    scn = lib.ref_read_scene(str(spath).encode())
+    assert scn, "reference could not read the mirror scene"
+    bpath = Path("/tmp/mirrors_ref.yrtbvh")
+    lib.ref_write_bvh(scn, str(bpath).encode())
+    rpath = Path("/tmp/mirrors_ref.yrtscene")
+    lib.ref_write_scene(scn, str(rpath).encode())
+    assert gzip.open(rpath).read() == gzip.open(spath).read(), "reference read-back differs"
+    dig = json.loads((HERE / "ref_digests.json").read_text())
+    dig["mirrors"] = {"scene_sha256": hashlib.sha256(gzip.open(spath).read()).hexdigest(),
+                      "bvh_sha256": hashlib.sha256(gzip.open(bpath).read()).hexdigest()}
+    (HERE / "ref_digests.json").write_text(json.dumps(dig, indent=1) + "\n")
+    out = {}
+    for res, sp in MIRROR_RENDERS:
+        w, h = C.c_int(), C.c_int()
+        lib.ref_image_size(scn, res, C.byref(w), C.byref(h))
+        img = np.zeros((h.value, w.value, 4), np.float32)
+        out[f"rays_r{res}_s{sp}"] = np.int64(lib.ref_render(scn, 0.1, res, sp, img.ctypes.data))
+        out[f"img_r{res}_s{sp}"] = img
+        print("mirrors", res, sp, "rays per camera sample", out[f"rays_r{res}_s{sp}"] / (h.value * w.value * sp * sp))
+    np.savez_compressed(HERE / "ref_render_mirrors.npz", **out)
+    rays = sample_rays(lib, scn, np.random.default_rng(37))
+    hit, inst, ei, ew, dist = trace(lib, scn, rays, False)
+    ahit = trace(lib, scn, rays, True)[0]
+    np.savez_compressed(HERE / "ref_rays_mirrors.npz", rays=rays, hit=hit, inst=inst, ei=ei, ew=ew, dist=dist,
+                        any_hit=ahit)
+    print("mirrors", dig["mirrors"], "hit fraction", hit.mean())
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["mirrors"]:
+        make_mirrors()
+    else:
+        main()
+        make_mirrors()

@@ -14,9 +14,15 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent.parent
 GOLDEN = ROOT / "tests" / "golden"
 SCENES = GOLDEN / "scenes"
-# the reference's four `in/*` scenes + "lines", a synthetic lines/points/texture scene
-# built by tests/golden/make_synthetic.py and rendered by the reference itself
-SCENE_NAMES = ("basic", "simple", "refl", "instance10000", "lines")
+# the reference's four `in/*` scenes + "lines", a synthetic lines/points/texture scene,
+# and "mirrors", a mirror corridor whose paths recurse 20-40 levels deep (both built by
+# tests/golden/make_synthetic.py) + the instance-scaling scenes (instance10000's `i`-line
+# pattern with 1 000 / 100 000 instances, tests/golden/make_scaling.py), all loaded,
+# rendered and traced by the reference itself
+SCENE_NAMES = ("basic", "simple", "refl", "instance10000", "lines", "instance1k", "instance100k", "mirrors")
+# the max_depth the GPU renders the mirror corridor with (its deepest path: 37-40 levels;
+# the reference's recursion has no cap)
+MIRROR_DEPTH = 64
 OBJ_SCENES = ("basic", "simple", "refl", "instance10000")
 REFERENCE = Path("/root/reference")
 REF_OBJ = {

@@ -264,3 +264,68 @@ def test_full_size_c5_properties(yrt):
         seg = img[row:row + 1, x0:x0 + 64]
         assert close_mask(seg, ref).all(), f"row {row} x0 {x0}"
         assert np.mean(seg.view(np.uint32) == ref.view(np.uint32)) > 0.99
+
+
+# ---- instance scaling (instance10000's `i`-line pattern, 1 K / 100 K) ----
+
+@pytest.mark.parametrize("name,ninst,depth", [("instance1k", 1004, 10), ("instance100k", 100004, 18)])
+def test_instance_scaling_c4_frame(yrt, name, ninst, depth):
+    """the scaling scenes at c4's settings (1920x1080, 8x8 spp): every camera sample traces
+    one ray and every hit one shadow ray per light, nothing is truncated or overflows, the
+    instance BVH depth plus the deepest shape BVH (15) stays within the walks' stack
+    (traversal_stack_cap = 40), and four whole rows equal the oracle"""
+    s = host_scene(yrt, name)
+    info = s.info()
+    assert info["instances"] == ninst and info["bvh_depth"] == depth and info["shape_bvh_depth"] == 15
+    assert depth + 15 <= 40
+    img, st = yrt.raytrace(s.upload(0), (0.1, 0.1, 0.1), 1080, 8, return_stats=True)
+    assert img.shape == (1080, 1920, 4)
+    assert st["camera_samples"] == 1920 * 1080 * 64
+    assert st["rays"] == st["camera_samples"] + st["shadow_rays"] and st["shadow_rays"] % 3 == 0
+    assert st["depth_truncated"] == 0 and st["stack_overflow"] == 0
+    rows = np.array([0, 377, 540, 1079], np.int32)
+    ref, _, trunc = Oracle(name).render(1080, 8, rows=rows)
+    assert trunc == 0
+    assert close_mask(img[rows], ref).all()
+    assert np.mean(img[rows].view(np.uint32) == ref.view(np.uint32)) > 0.99
+
+
+def test_upload_rejects_bvh_deeper_than_the_stack(yrt):
+    """instances on an exponential sequence make the reference's midpoint split peel one
+    instance per level: an instance BVH 49 deep, past traversal_stack_cap (40), which the
+    upload refuses (YRT_ERR_UNSUPPORTED) instead of letting a walk overflow its stack"""
+    s = yrt.Scene.create()
+    s.add_camera(np.r_[1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 1, 5], fovy=0.5, aspect=1.5, focus=5)
+    m = s.add_material(kd=(0.5, 0.5, 0.5))
+    tri = s.add_shape([[-1, 0, -1], [1, 0, -1], [0, 0, 1]], norm=[[0, 1, 0]] * 3, texcoord=[[0, 0]] * 3,
+                      triangles=[[0, 1, 2]])
+    for k in range(80):
+        s.add_instance(np.r_[1, 0, 0, 0, 1, 0, 0, 0, 1, 2.0 ** k, 0, 0], tri, m)
+    yrt.build_bvh(s)
+    assert s.info()["bvh_depth"] > 40
+    with pytest.raises(yrt.YrtError, match="too deep"):
+        s.upload(0)
+
+
+# ---- mirror recursion deeper than 16 levels (the reference's recursion has no cap) ----
+
+def test_mirror_corridor_deep_recursion(yrt):
+    """tests/golden/scenes/mirrors.yrtscene: camera rays bounce between two mirror walls
+    up to 37-40 times. With max_depth 64 the wavefront pipeline keeps every level's records
+    in HBM and the whole 640x360x4 frame equals the oracle's unbounded recursion (ray
+    count included, nothing truncated); with max_depth 30 the cut paths count as misses,
+    exactly as the oracle's depth cap counts them"""
+    s = host_scene(yrt, "mirrors")
+    ds = s.upload(0)
+    o = Oracle("mirrors")
+    ref, nrays, trunc = o.render(360, 2)
+    assert trunc == 0
+    img, st = yrt.raytrace(ds, (0.1, 0.1, 0.1), 360, 2, max_depth=64, return_stats=True)
+    assert st["depth_truncated"] == 0 and st["rays"] == nrays
+    assert nrays / st["camera_samples"] > 60  # ~26 levels of 1 + 2 shadow rays on average
+    assert close_mask(img, ref).all()
+    assert np.mean(img.view(np.uint32) == ref.view(np.uint32)) > 0.99
+    ref30, n30, t30 = o.render(360, 2, max_depth=30)
+    img30, st30 = yrt.raytrace(ds, (0.1, 0.1, 0.1), 360, 2, max_depth=30, return_stats=True)
+    assert t30 > 0 and st30["depth_truncated"] == t30 and st30["rays"] == n30
+    assert close_mask(img30, ref30).all()

@@ -460,6 +460,9 @@ int yrt_render(yrt_scene* s, const yrt_render_params* p, float* out, int mem, vo
         hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
         // timing 1: start a new record; 2: keep accumulating across calls (bench loops)
         if (!(p->timing == 2 && s->ds->timer.on)) s->ds->timer.reset(p->timing != 0);
+        if (p->algorithm == YRT_ALGO_MEGAKERNEL && s->ds->reflective && a.max_depth > yrt::megakernel_max_depth)
+            throw yrt::unsupported_error("the megakernel keeps " + std::to_string(yrt::megakernel_max_depth) +
+                                         " mirror levels per lane; deeper recursions need the wavefront algorithm");
         if (p->algorithm == YRT_ALGO_MEGAKERNEL)
             hip_check(yrt::launch_render(*s->ds, a, dst, s->counters, p->count_work != 0, st), "render kernel launch");
         else if (p->algorithm == YRT_ALGO_WAVEFRONT || p->algorithm == YRT_ALGO_WAVEFRONT_LANE)

@@ -18,10 +18,11 @@ namespace yrt {
 namespace {
 
 constexpr int BLOCK_X = 16, BLOCK_Y = 8, BLOCK = BLOCK_X * BLOCK_Y;
-constexpr int MAX_BOUNCES = 16;  // compile-time cap of the per-level shading records
+constexpr int MAX_BOUNCES = megakernel_max_depth;  // compile-time size of the per-level shading records
 
+template <typename SE>
 struct lane_state {
-    uint16_t* stk;
+    SE* stk;  // this lane's column of the LDS traversal stack (16- or 32-bit node indices)
     work_counts wc;
     unsigned long long rays = 0;
     unsigned long long truncated = 0;
@@ -30,8 +31,8 @@ struct lane_state {
 // shade() (raytrace.cpp:88-211) with the recursion unrolled: level k records its
 // light sum D_k, ambient la_k and kr_k; the result folds back to front as
 // R_k = (D_k + R_{k+1}*kr_k) + la_k, the reference's accumulation order (:182,203,206).
-template <bool COUNT>
-__device__ vec3f shade_path(const dev_scene_view& S, const dev_render_args& A, ray3 ray, lane_state& L) {
+template <bool COUNT, typename SE>
+__device__ vec3f shade_path(const dev_scene_view& S, const dev_render_args& A, ray3 ray, lane_state<SE>& L) {
     vec3f rec_d[MAX_BOUNCES], rec_la[MAX_BOUNCES], rec_kr[MAX_BOUNCES];
     int depth = 0;
     vec3f R = {0, 0, 0};
@@ -118,8 +119,8 @@ __device__ vec3f shade_path(const dev_scene_view& S, const dev_render_args& A, r
     return R;
 }
 
-template <bool COUNT>
-__device__ void flush_counters(unsigned long long* counters, const lane_state& L, unsigned long long samples) {
+template <bool COUNT, typename SE>
+__device__ void flush_counters(unsigned long long* counters, const lane_state<SE>& L, unsigned long long samples) {
     unsigned long long vals[9] = {L.rays, samples, L.truncated, 0, L.wc.box, L.wc.inst, L.wc.prim, L.wc.hits,
                                   L.wc.tex};
     int n = COUNT ? 9 : 3;
@@ -129,12 +130,14 @@ __device__ void flush_counters(unsigned long long* counters, const lane_state& L
     }
 }
 
-// raytrace() (raytrace.cpp:213-254) for the window/bands in A; one lane = one pixel
-template <bool COUNT>
+// raytrace() (raytrace.cpp:213-254) for the window/bands in A; one lane = one pixel.
+// SE: the stack entry type -- 16-bit node indices while every tree has < 65 536 nodes
+// (half the LDS), 32-bit otherwise (instance100k's instance tree has 67 727)
+template <bool COUNT, typename SE>
 __global__ __launch_bounds__(BLOCK) void render_kernel(dev_scene_view S, dev_render_args A,
                                                        float4* __restrict__ out, unsigned long long* counters) {
-    __shared__ uint16_t lds[traversal_stack_cap * BLOCK];
-    lane_state L;
+    __shared__ SE lds[traversal_stack_cap * BLOCK];
+    lane_state<SE> L;
     L.stk = lds + threadIdx.x;
     int lx = blockIdx.x * BLOCK_X + (threadIdx.x % BLOCK_X);
     int ly = blockIdx.y * BLOCK_Y + (threadIdx.x / BLOCK_X);
@@ -286,15 +289,22 @@ hipError_t launch_rgbe(const float* rgba, int w, int h, unsigned char* out, hipS
 hipError_t launch_render(device_scene& ds, const dev_render_args& args, void* out_rgba,
                          unsigned long long* counters, bool count_work, hipStream_t stream) {
     if (args.tile_w <= 0 || args.tile_h <= 0) return hipSuccess;
-    if (!ds.narrow_stack) return hipErrorNotSupported;  // megakernel keeps 16-bit stack entries
     dim3 grid((args.tile_w + BLOCK_X - 1) / BLOCK_X, (args.tile_h + BLOCK_Y - 1) / BLOCK_Y);
     int t = ds.timer.begin(phase_megakernel, stream);
-    if (count_work)
-        hipLaunchKernelGGL(render_kernel<true>, grid, dim3(BLOCK), 0, stream, ds.view, args, (float4*)out_rgba,
-                           counters);
-    else
-        hipLaunchKernelGGL(render_kernel<false>, grid, dim3(BLOCK), 0, stream, ds.view, args, (float4*)out_rgba,
-                           counters);
+#define YRT_MK(C, SE) \
+    hipLaunchKernelGGL((render_kernel<C, SE>), grid, dim3(BLOCK), 0, stream, ds.view, args, (float4*)out_rgba, counters)
+    if (ds.narrow_stack) {
+        if (count_work)
+            YRT_MK(true, uint16_t);
+        else
+            YRT_MK(false, uint16_t);
+    } else {
+        if (count_work)
+            YRT_MK(true, uint32_t);
+        else
+            YRT_MK(false, uint32_t);
+    }
+#undef YRT_MK
     ds.timer.end(t, stream);
     return hipGetLastError();
 }

@@ -58,7 +58,6 @@ constexpr int shadow_block() { return PACKET ? YRT_SHADOW_BLOCK : WF_BLOCK; }
 #ifndef YRT_SHADOW_GRAB
 #define YRT_SHADOW_GRAB 8  // k_shadow_persist: queue positions taken per atomic (A/B: 2 / 4 / 8 / 32: +82 / -0.8 / -1.9 / +2.4 %)
 #endif
-constexpr int MAX_LEVELS = 16;
 constexpr int CHUNK_LOG2 = 29;  // samples per chunk, non-reflective scenes (~70 B of HBM each)
 constexpr int TILE = 8;         // pixel tiles of TILE x TILE in the sample enumeration
 
@@ -69,12 +68,19 @@ struct wf_buffers {
     unsigned char* occl;  // [light][sample]
     f4* rad;            // level-0 radiance per sample
     // bounce levels (reflective scenes only)
-    f4* ray_o[MAX_LEVELS];  // level k >= 1: {o.xyz, parent index}
-    f4* ray_d[MAX_LEVELS];  // level k >= 1: {d.xyz, -}
-    f4* rec0[MAX_LEVELS];   // level k: {D.xyz, child index}
-    f4* rec1[MAX_LEVELS];   // {la.xyz, -}
-    f4* rec2[MAX_LEVELS];   // {kr.xyz, -}
-    int* count;             // count[k]: rays at level k (k >= 1)
+    // mirror levels (reflective scenes): one slab per record kind, `capacity` records per
+    // level, so any number of levels is plain indexing (the reference recursion has no cap)
+    f4* ray_o_;  // level k >= 1 at (k - 1) * capacity: {o.xyz, parent index}
+    f4* ray_d_;  // level k >= 1: {d.xyz, -}
+    f4* rec0_;   // level k < nlevels - 1 at k * capacity: {D.xyz, child index}
+    f4* rec1_;   // {la.xyz, -}
+    f4* rec2_;   // {kr.xyz, -}
+    __device__ __forceinline__ f4* ray_o(int k) const { return ray_o_ + (size_t)(k - 1) * capacity; }
+    __device__ __forceinline__ f4* ray_d(int k) const { return ray_d_ + (size_t)(k - 1) * capacity; }
+    __device__ __forceinline__ f4* rec0(int k) const { return rec0_ + (size_t)k * capacity; }
+    __device__ __forceinline__ f4* rec1(int k) const { return rec1_ + (size_t)k * capacity; }
+    __device__ __forceinline__ f4* rec2(int k) const { return rec2_ + (size_t)k * capacity; }
+    int* count;             // count[k]: rays at level k (k >= 1), nlevels + 1 entries
     unsigned* queue;        // per-XCD work counters of the persistent shadow kernel: [0, 8)
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
         const bool valid = idx < n;
         ray3 ray = {{0, 0, 0}, {0, 0, 1}, ray_eps, flt_max};
         if (valid) {
-            float4 o = ld4(B.ray_o[level] + idx), d = ld4(B.ray_d[level] + idx);
+            float4 o = ld4(B.ray_o(level) + idx), d = ld4(B.ray_d(level) + idx);
             ray = {xyz(o), xyz(d), ray_eps, flt_max};
             rays++;
         }
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 const vec3f nrm = xyz(s1);
                 const vec2f uv = {s1.w, B.surfv[idx]};
                 const int mat = info >> 2, kind = info & 3;
-                const vec3f ro = level ? xyz(ld4(B.ray_o[level] + idx)) : cam_o;
+                const vec3f ro = level ? xyz(ld4(B.ray_o(level) + idx)) : cam_o;
                 float4 m0, m1, m2, m3;
                 {
                     m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1);
@@ -596,9 +602,9 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 vec3f col = R;
                 int lev = level, node = idx;
                 while (lev > 0) {
-                    const int parent = ibits(B.ray_o[lev][node].w);
-                    const float4 d = ld4(B.rec0[lev - 1] + parent), la = ld4(B.rec1[lev - 1] + parent),
-                                 kr = ld4(B.rec2[lev - 1] + parent);
+                    const int parent = ibits(B.ray_o(lev)[node].w);
+                    const float4 d = ld4(B.rec0(lev - 1) + parent), la = ld4(B.rec1(lev - 1) + parent),
+                                 kr = ld4(B.rec2(lev - 1) + parent);
                     vec3f cc = {d.x, d.y, d.z};
                     cc = cc + vec3f{col.x * kr.x, col.y * kr.y, col.z * kr.z};
                     cc = cc + xyz(la);
@@ -625,11 +631,11 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
         __syncthreads();
         if (spawn) {
             const int slot = cmp_base[w] + __popcll(mask & ((1ull << lane) - 1));
-            B.ray_o[level + 1][slot] = {p.x, p.y, p.z, __int_as_float(idx)};
-            B.ray_d[level + 1][slot] = {dr.x, dr.y, dr.z, 0};
-            B.rec0[level][idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
-            B.rec1[level][idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
-            B.rec2[level][idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
+            B.ray_o(level + 1)[slot] = {p.x, p.y, p.z, __int_as_float(idx)};
+            B.ray_d(level + 1)[slot] = {dr.x, dr.y, dr.z, 0};
+            B.rec0(level)[idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
+            B.rec1(level)[idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
+            B.rec2(level)[idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
         }
     }
     if (FUSE) {
@@ -705,10 +711,10 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
-    size_t b = align_up(sizeof(int) * (MAX_LEVELS + 1)) + align_up(16 * sizeof(unsigned));
+    size_t b = align_up(sizeof(int) * (size_t)(nlevels + 1)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
-    // levels >= 1: ray_o, ray_d; levels < last: rec0..2
-    if (nlevels > 1) b += (size_t)(nlevels - 1) * 2 * align_up(16 * c) + (size_t)(nlevels - 1) * 3 * align_up(16 * c);
+    // levels >= 1: ray_o, ray_d; levels < last: rec0..2 (one slab each)
+    if (nlevels > 1) b += 5 * align_up((size_t)(nlevels - 1) * 16 * c);
     return b;
 }
 
@@ -721,21 +727,20 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
         p += align_up(bytes);
         return (void*)q;
     };
-    B.count = (int*)take(sizeof(int) * (MAX_LEVELS + 1));
+    B.count = (int*)take(sizeof(int) * (size_t)(nlevels + 1));
     B.queue = (unsigned*)take(16 * sizeof(unsigned));
     B.surf0 = (f4*)take(16 * c);
     B.surf1 = (f4*)take(16 * c);
     B.surfv = (float*)take(4 * c);
     B.occl = (unsigned char*)take(c * std::max(nlights, 1));
     B.rad = (f4*)take(16 * c);
-    for (int k = 1; k < nlevels; k++) {
-        B.ray_o[k] = (f4*)take(16 * c);
-        B.ray_d[k] = (f4*)take(16 * c);
-    }
-    for (int k = 0; k + 1 < nlevels; k++) {
-        B.rec0[k] = (f4*)take(16 * c);
-        B.rec1[k] = (f4*)take(16 * c);
-        B.rec2[k] = (f4*)take(16 * c);
+    if (nlevels > 1) {
+        const size_t slab = (size_t)(nlevels - 1) * 16 * c;
+        B.ray_o_ = (f4*)take(slab);
+        B.ray_d_ = (f4*)take(slab);
+        B.rec0_ = (f4*)take(slab);
+        B.rec1_ = (f4*)take(slab);
+        B.rec2_ = (f4*)take(slab);
     }
     B.capacity = cap;
     B.nlevels = nlevels;
@@ -749,10 +754,13 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     const int tiles_x = (A.tile_w + TILE - 1) / TILE;
     const int tiles_y = (A.tile_h + TILE - 1) / TILE;
     const long long npix_total = (long long)tiles_x * tiles_y * TILE * TILE;
-    const int nlevels = ds.reflective ? std::min(std::max(A.max_depth, 1), MAX_LEVELS) : 1;
+    // one level per trace_first call a camera sample may make (A.max_depth; the reference
+    // recursion is unbounded, so the caller's depth is kept as given)
+    const int nlevels = ds.reflective ? std::max(A.max_depth, 1) : 1;
     // samples per chunk: a whole frame at c3/c4, 15 chunks at c5. A reflective scene keeps
-    // per-level buffers for every level (~100 B per sample and level). The chunk is
-    // halved until the workspace takes at most half of the free HBM.
+    // per-level records for every level (80 B per sample and level). The chunk is halved
+    // until the workspace takes at most half of the free HBM (deep mirror recursions run
+    // as more, smaller chunks).
     long long target = ds.reflective ? (1ll << 25) : (1ll << CHUNK_LOG2);
     auto cap_for = [&](long long tgt) {
         int pix = (int)std::max<long long>(1, std::min<long long>(npix_total, tgt / spp));
@@ -766,7 +774,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         free_b += ds.work_bytes;  // the current workspace is given back if it is regrown
-        while (target > (1ll << 20) && workspace_bytes((int)target, ds.nlights, nlevels) > free_b / 2) target /= 2;
+        while (target > (1ll << 16) && workspace_bytes((int)target, ds.nlights, nlevels) > free_b / 2) target /= 2;
         pix_per_chunk = cap_for(target);
     }
     const int cap = pix_per_chunk * spp;
@@ -790,7 +798,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         const int nsamp = C.npix * spp;
         const int grid = (nsamp + WF_BLOCK - 1) / WF_BLOCK;
         if (nlevels > 1) {
-            hipError_t e = hipMemsetAsync(B.count, 0, sizeof(int) * (MAX_LEVELS + 1), stream);
+            hipError_t e = hipMemsetAsync(B.count, 0, sizeof(int) * (size_t)(nlevels + 1), stream);
             if (e != hipSuccess) return e;
         }
         int t = T.begin(phase_primary, stream);

@@ -88,6 +88,10 @@ hipError_t launch_tonemap(const float* rgba, int n, unsigned char* out, const to
 // the .hdr writer's RGBE bytes on the device (rgbe.h; the layout of rgbe_encode)
 hipError_t launch_rgbe(const float* rgba, int w, int h, unsigned char* out, hipStream_t stream);
 
+// mirror levels the megakernel records per lane (render.hip); the wavefront pipeline
+// keeps per-level records in HBM and takes any max_depth
+constexpr int megakernel_max_depth = 16;
+
 // traversal stack entries per lane (LDS resident): instance level + shape level
 constexpr int traversal_stack_cap = 40;
 
