@@ -11,7 +11,10 @@ point), pinned by the REFERENCE ITSELF:
 2. has the reference read that file into its own structs (oracle/_ref
    ref_read_scene -> scene.h types + build_bvh, scene.cpp:554) and render / trace it
    (raytrace.cpp:213, scene.cpp:483-494), writing `ref_render_lines.npz`,
-   `ref_rays_lines.npz` and the scene/BVH digests into `ref_digests.json`.
+   `ref_rays_lines.npz` and the scene/BVH digests into `ref_digests.json`;
+3. does the same for `scenes/mirrors.yrtscene` (`... make_synthetic.py mirrors` for it
+   alone): a mirror corridor whose camera rays bounce 37-40 times, deeper than any
+   `in/*` scene (the reference's recursion has no depth cap).
 
 Data only; no reference source is copied.
 """
@@ -170,8 +173,8 @@ MIRROR_DEPTH = 64  # the GPU's max_depth for these fixtures (the reference has n
 def build_mirrors(path: Path):
     """A mirror corridor: two parallel mirror walls 2 apart along x in [0, 100], a
     diffuse floor, two point lights, and a camera between the walls turned 30 degrees
-    toward one of them, so that camera rays bounce between the walls ~20-36 times before
-    they leave the corridor (past the reference-free 16-level cap of round 2)."""
+    toward one of them, so that camera rays bounce between the walls 20-40 times before
+    they leave the corridor (past round 2's 16-level cap)."""
     import yocto_raytracing_amd as yrt
 
     s = yrt.Scene.create()
