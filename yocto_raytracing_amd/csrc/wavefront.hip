@@ -475,152 +475,6 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     flush_block<1, SP_BLOCK>(counters, {cnt_shadow_rays}, {mine});
 }
 
-#ifndef YRT_FUSE_SHADE
-#define YRT_FUSE_SHADE 0  // s = 8, no mirrors: shadow rays and shading of a pixel in one persistent kernel (A/B)
-#endif
-#if YRT_FUSE_SHADE
-// ---- shadow rays + shade() + the pixel's ordered sum, one 64-sample pixel per wave ----
-// (s = 8, a scene without mirrors). A wave takes the next pixel of its XCD's queue, walks
-// the pixel's shadow rays to every light in light order (packet_occluded_wide2, the
-// occlusion kept as one bit per light in a register), shades its 64 samples as k_shade
-// does (raytrace.cpp:99-182) and sums them in the reference's order (:232-249) from LDS:
-// no occlusion bytes, no second surface read, no separate launch.
-constexpr unsigned FS_RUN = 8;  // pixels per XCD run
-__global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_shade(dev_scene_view S, dev_render_args A,
-                                                                              chunk_args C, int nsamp, wf_buffers B,
-                                                                              unsigned long long* counters,
-                                                                              float4* __restrict__ out) {
-    constexpr int WPB = SP_BLOCK / 64;
-    __shared__ float rad[WPB][3][64];
-    const int nl = S.nlights;
-    const unsigned n_items = (unsigned)(nsamp + 63) / 64u;  // pixels
-    const unsigned wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const unsigned xcd = blockIdx.x % 8u;
-    const unsigned full = n_items / (8u * FS_RUN) * (8u * FS_RUN);
-    const unsigned per_xcd = full / 8u;
-    unsigned rays = 0;
-    auto issue = [&]() -> unsigned {
-        unsigned v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return v;
-    };
-    constexpr unsigned G = YRT_SHADOW_GRAB;
-    unsigned qv = issue();
-    unsigned qb = 0, qleft = 0;
-    const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
-    const vec3f cam_o = {A.cam.ox, A.cam.oy, A.cam.oz};
-    for (;;) {
-        if (qleft == 0) {
-            qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
-            qleft = G;
-            qv = issue();
-        }
-        qleft--;
-        const unsigned q = qb++;
-        const unsigned it = q < per_xcd ? ((q / FS_RUN) * 8u + xcd) * FS_RUN + q % FS_RUN : full + (q - per_xcd) * 8u + xcd;
-        if (it >= n_items) break;
-        const int idx = (int)it * 64 + (int)lane;
-        float4 s0 = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-2));
-        if (idx < nsamp) s0 = ld4(B.surf0 + idx);
-        const int info = ibits(s0.w);
-        const vec3f p = xyz(s0);
-        uint32_t occ_bits = 0;
-        for (int li = 0; li < nl; li++) {
-            const f4* lr = S.lights + 6 * li;
-            const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
-            const vec3f lp0 = xyz(ld4(lr + 4));
-            bool valid = false;
-            ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
-            if (info >= 0) {
-                vec3f tp = transform_point(lf, lp0 - p);
-                vec3f l = normalize(tp);
-                float r = length(tp);
-                sr = {p, l, 0.01f, r - 0.01f};
-                valid = true;
-            }
-            rays += (unsigned)__popcll(ballot(valid));
-            const bool occ = packet_occluded_wide2<0>(S, sr, valid, nullptr);
-            occ_bits |= occ ? 1u << li : 0u;
-        }
-        vec3f R = {0, 0, 0};
-        if (info >= 0) {
-            const float4 s1 = ld4(B.surf1 + idx);
-            const vec3f nrm = xyz(s1);
-            const vec2f uv = {s1.w, B.surfv[idx]};
-            const int mat = info >> 2, kind = info & 3;
-            const float4 m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1), m2 = ld4(S.mats + 4 * mat + 2);
-            const vec3f kd0 = xyz(m0), ks0 = xyz(m1);
-            const float ns = m0.w;
-            const int kd_txt = ibits(m1.w), ks_txt = ibits(m2.w);
-            work_counts wc;
-            vec3f la = amb * kd0;
-            vec3f tkd = {1, 1, 1}, tks = {1, 1, 1};
-            if (kd_txt >= 0) {
-                tkd = eval_texture<false>(S, kd_txt, uv, wc);
-                la = la * tkd;
-            }
-            if (ks_txt >= 0) tks = eval_texture<false>(S, ks_txt, uv, wc);
-            vec3f c = {0.0f, 0.0f, 0.0f};
-            const vec3f v = normalize(cam_o - p);
-            for (int li = 0; li < nl; li++) {
-                if ((occ_bits >> li) & 1u) continue;
-                float4 lrec[6];
-                ld_scalar<6>(S.lights + 6 * li, lrec);
-                frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
-                vec3f lp0 = xyz(lrec[4]), ke = xyz(lrec[5]);
-                vec3f tp = transform_point(lf, lp0 - p);
-                vec3f l = normalize(tp);
-                float r = length(tp);
-                vec3f h = normalize(v + l);
-                vec3f kd = kd0, ks = ks0;
-                if (kd_txt >= 0) kd = kd * tkd;
-                if (ks_txt >= 0) ks = ks * tks;
-                vec3f ld = kd * (ke / (r * r));
-                vec3f ls = ks * (ke / (r * r));
-                if (kind == kind_lines) {
-                    float prodnl = dot(nrm, l);
-                    float prodnh = dot(nrm, h);
-                    if (prodnl < 0.0f) prodnl *= -1;
-                    if (prodnh < 0.0f) prodnh *= -1;
-                    float sinnl = __builtin_sqrtf(1.0f - prodnl);
-                    float sinnh = __builtin_sqrtf(1.0f - prodnh);
-                    ld = ld * sinnl;
-                    ls = ls * spec_pow(sinnh, ns, ls);
-                } else {
-                    ld = ld * smax(0.0f, dot(nrm, l));
-                    ls = ls * spec_pow(smax(0.0f, dot(nrm, h)), ns, ls);
-                }
-                c = c + (ld + ls);
-            }
-            R = c + la;
-        }
-        rad[wv][0][lane] = R.x, rad[wv][1][lane] = R.y, rad[wv][2][lane] = R.z;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (lane < 3) {
-            // raytrace.cpp:232-249: the pixel's 64 samples in jj/ii order, then / 64
-            int lx, ly, i, j;
-            const long long pl = (long long)it;
-            const bool valid = pl < C.npix && pixel_of(A, C.tiles_x, C.pix0 + pl, lx, ly, i, j);
-            if (pl < C.npix && lx < A.tile_w && ly < A.tile_h) {
-                float vsum = 0.0f;
-                if (valid) {
-                    float acc = 0.0f;
-                    for (int k = 0; k < 64; k++) acc = acc + rad[wv][lane][k];
-                    vsum = acc / 64.0f;
-                }
-                float* o = reinterpret_cast<float*>(out + (size_t)ly * A.out_stride + lx);
-                o[lane] = vsum;
-                if (lane == 0) o[3] = valid ? 1.0f : 0.0f;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
-    flush_block<1, SP_BLOCK>(counters, {cnt_shadow_rays}, {mine});
-}
-#endif
-
 // ---- shade() after the queries (raytrace.cpp:99-206) ----
 // FUSE (level 0 of a scene without mirrors, s*s dividing the block): the block's
 // samples are whole pixels, so the ordered per-pixel sum of k_accumulate is done here
@@ -970,18 +824,6 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                    level, B, counters);
                 T.end(t, stream);
             }
-#if YRT_FUSE_SHADE
-            if (!COUNT && PACKET && ds.wide_ok && nlevels == 1 && spp == 64 && ds.nlights > 0 && ds.nlights <= 32) {
-                t = T.begin(phase_shadow, stream);
-                const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
-                hipError_t e = hipMemsetAsync(B.queue, 0, 8 * sizeof(unsigned), stream);
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(k_shadow_shade, dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view, A, C, nsamp, B, counters,
-                                   out);
-                T.end(t, stream);
-                break;  // one level; shaded and summed
-            }
-#endif
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
