@@ -144,23 +144,6 @@ __device__ __forceinline__ void ld_records_at(const f4* base, unsigned index, fl
 }
 
 
-#ifndef YRT_FIRST_APRIMS
-#define YRT_FIRST_APRIMS 0  // closest hit: triangles from the packed aprims array, the element index only on a hit
-#endif
-// a triangle's v0, e1, e2 from the packed 9-float array (yrt_device.h aprims): s_load_dwordx8
-// + s_load_dword, 9 SGPRs instead of the 48-byte sprims record's 12
-__device__ __forceinline__ void ld_aprim(const dev_scene_view& S, int i, vec3f& v0, vec3f& e1, vec3f& e2) {
-    const f4* abase = sgpr_ptr(reinterpret_cast<const f4*>(S.aprims));
-    sgpr8 a;
-    int b;
-    asm volatile("s_load_dwordx8 %0, %2, %3\n s_load_dword %1, %2, %3 offset:0x20\n s_waitcnt lgkmcnt(0)"
-                 : "=&s"(a), "=&s"(b)
-                 : "s"(abase), "s"(uniform(i * 36)));
-    v0 = {__int_as_float(a[0]), __int_as_float(a[1]), __int_as_float(a[2])};
-    e1 = {__int_as_float(a[3]), __int_as_float(a[4]), __int_as_float(a[5])};
-    e2 = {__int_as_float(a[6]), __int_as_float(a[7]), __int_as_float(b)};
-}
-
 // intersect_triangle (scene.cpp:229-263) without branches: the same values in the
 // same order; the early returns become one predicate (a NaN w1/w2/t passes its
 // range checks exactly as it does in the reference).
@@ -603,32 +586,19 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 DBG_CHECK(lstart >= 0 && lstart + lcount <= S.nsprims, 2, lstart, lcount, level, kind, sp);
                 if (kind == kind_triangles) {
                     for (int i = lstart; i < lstart + lcount; i++) {
-#if YRT_FIRST_APRIMS
-                        vec3f tv0, te1, te2;
-                        ld_aprim(S, i, tv0, te1, te2);
-#else
                         float4 pv[3];
                         ld_records_at<3>(S.sprims, (unsigned)(3 * i), pv);
-                        const vec3f tv0 = xyz(pv[0]), te1 = xyz(pv[1]), te2 = xyz(pv[2]);
-#endif
                         if (COUNT && in) wc.prim++;
                         if (COUNT && (me & 1)) wc.wprim++;
                         float t, w1, w2;
-                        const bool h = tri_hit_nb<true>(co, cd, tmin, tmax, tv0, te1, te2, t, w1, w2, in, lmask) && in;
+                        const bool h = tri_hit_nb<true>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t,
+                                                        w1, w2, in, lmask) &&
+                                       in;
                         // most triangles hit no lane: their record-keeping selects are skipped
                         if (ballot(h)) {
-#if YRT_FIRST_APRIMS
-                            // the element index (sprims row 0 .w) only for a triangle that some lane hits
-                            int ei;
-                            asm volatile("s_load_dword %0, %1, %2 offset:0xc\n s_waitcnt lgkmcnt(0)"
-                                         : "=s"(ei)
-                                         : "s"(sgpr_ptr(S.sprims)), "s"(uniform(i * 48)));
-#else
-                            const int ei = ibits(pv[0].w);
-#endif
                             tmax = h ? t : tmax;
                             hslot = h ? cur_slot : hslot;
-                            hei = h ? ei : hei;
+                            hei = h ? ibits(pv[0].w) : hei;
                             hw1 = h ? w1 : hw1;
                             hw2 = h ? w2 : hw2;
                             leaf_hit |= h ? 1 : 0;
