@@ -438,7 +438,10 @@ def main():
         metric = BASELINE_METRIC if is_c4 else f"Mrays/sec + ms/frame, {a.scene} {W}×{H}×{spp}spp, {world} MI355X"
         key = f"{a.scene}-{W}x{H}-s{a.samples}-n{band_world}-{a.algorithm}-{dom}"
         kernel_ms = dom_ms / dom_launches
-        identity = code_identity(yrt_native.LIB_PATH)
+        try:
+            identity = code_identity(yrt_native.LIB_PATH)
+        except (OSError, ValueError, subprocess.CalledProcessError) as e:  # no binutils/bundler: no roofline
+            identity = f"unavailable ({type(e).__name__})"
         tr, _ = load_counters(Path(a.traffic_json), key, identity)
         traffic = tr.get("hbm_bytes_per_launch") if tr else None
         key_n1 = f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-{dom}"

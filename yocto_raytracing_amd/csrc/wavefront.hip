@@ -412,18 +412,16 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         nx = (nsamp + 63) / 64;
     }
     const unsigned n_items = (unsigned)nx * (unsigned)nl;
-    const unsigned wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
-    (void)wv;
     const unsigned full = n_items / (8u * C) * (8u * C);     // items in whole super-runs
     const unsigned per_xcd = full / 8u;
     unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays traced by this wave
     // the waves of an XCD take the positions of its item sequence from one agent-scope
     // counter (one atomic per batch, issued a batch ahead), which keeps the chip's working
     // window as tight as the hardware's block dealing does (a fixed interleave, wave j
-    // taking j, j + W, ..., lets the waves drift apart: +21 %); the atomic's result stays in lane 0's VGPR until the next item needs it: it is
-    // issued after this item's surface load and before its walk (the walk reads only
-    // through the scalar cache), so its latency hides behind the walk
+    // taking j, j + W, ..., lets the waves drift apart: +21 %). The atomic's result stays
+    // in lane 0's VGPR until the next batch needs it, so its latency hides behind the walks
     auto issue = [&]() -> unsigned {
         unsigned v = 0;
         if (lane == 0) v = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
