@@ -79,6 +79,8 @@ def parse():
     p.add_argument("--profile-rank", default="",
                    help="R/N: one process renders rank R's bands of an N-rank run, no gather (the counter "
                         "passes for the N-rank roofline, tools/gpu_issue_pmc.sh); its line is not a bench result")
+    p.add_argument("--no-count-pass", action="store_true",
+                   help="skip the untimed instrumented pass that gives SURVEY §8(d)'s algorithmic bytes")
     p.add_argument("--dry-run", action="store_true",
                    help="launch/rendezvous/report only, no GPU work (tests the N-rank launcher on CPU)")
     return p.parse_args()
@@ -226,6 +228,13 @@ def cpu_baseline_all_cores(scene_file: Path, res: int, width: int, spp_axis: int
 
 
 # ---------------------------------------------------------------- roofline
+
+def algorithmic_bytes(st: dict, pixels: int) -> float:
+    """SURVEY §8(d)'s fixed yardstick: the reference's traversal and shading work on its
+    own AoS layout, in bytes"""
+    return float(32 * st["box_tests"] + 56 * st["instance_entries"] + 52 * st["prim_tests"] +
+                 216 * st["shaded_hits"] + 16 * st["texture_lookups"] + 16 * pixels)
+
 
 def frame_digest(frame) -> str:
     """sha256 of a float32 RGBA frame's bytes in image order (host copy, untimed)"""
@@ -424,13 +433,24 @@ def main():
     if rank == 0 and not a.profile_rank:
         frame_sha256 = frame_digest(frames[b])
 
+    # SURVEY §8(d)'s algorithmic yardstick, from one instrumented (untimed) pass of this
+    # rank's share: the reference's work counts x the reference layout's bytes per unit
+    algo_bytes = 0.0
+    if not a.no_count_pass:
+        params.count_work, params.timing = 1, 0
+        ds.render_into(params, shards[0].data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        algo_bytes = algorithmic_bytes(ds.last_stats(), local_rows * W)
+        params.count_work = 0
+
     t = torch.tensor([elapsed, dom_ms, render_ms, e2e_ms], dtype=torch.float64, device=dev)
-    rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps], dtype=torch.float64, device=dev)
+    rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps, algo_bytes], dtype=torch.float64,
+                        device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
     elapsed, dom_ms, render_ms, e2e_ms = (float(v) for v in t)
-    total_rays, total_samples = float(rays[0]), float(rays[1])
+    total_rays, total_samples, total_algo_bytes = float(rays[0]), float(rays[1]), float(rays[2])
 
     if rank == 0:
         spp = a.samples * a.samples
@@ -491,6 +511,16 @@ def main():
                        "camera_Msamples_per_s": total_samples / elapsed / 1e6,
                        "algorithm": a.algorithm},
             "roofline": roof,
+            "algorithmic_yardstick": None if a.no_count_pass else {
+                "bytes_per_frame": total_algo_bytes,
+                "GBs": total_algo_bytes / (elapsed / a.steps) / 1e9,
+                "frac_of_hbm_peak": total_algo_bytes / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS / world,
+                "note": ("SURVEY §8(d): 32 B per box test, 56 B per instance entry, 52 B per primitive test, "
+                         "216 B per shaded hit, 16 B per texture lookup, 16 B per pixel, with the reference's "
+                         "own work counts (one instrumented pass, untimed), over the timed ms/frame. The "
+                         "reference's per-ray fetches of its AoS layout, not this path's traffic: the packet "
+                         "walks fetch each record once per 64-ray wave from a cache-resident scene, so this "
+                         "exceeds the HBM peak; roofline above is the bound that applies.")},
             "frame_sha256": frame_sha256,
         }
         if a.profile_rank:  # a counter-collection run, not a bench result

@@ -9,7 +9,7 @@ TAG=$1; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-B="bench.py --steps 1 --warmup 0 --cpu-seconds 0 $*"
+B="bench.py --steps 1 --warmup 0 --cpu-seconds 0 --no-count-pass $*"
 groups=(
   "SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_SMEM SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
   "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"
