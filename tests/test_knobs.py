@@ -29,6 +29,7 @@ VARIANTS = {
     "YRT_TRACE_WAVES": ["-DYRT_TRACE_WAVES=7"],
     "YRT_SHADOW_WAVES": ["-DYRT_SHADOW_WAVES=6"],
     "YRT_SHADE_WAVES": ["-DYRT_SHADE_WAVES=5"],
+    "YRT_SHADE_LDS_SRGB": ["-DYRT_SHADE_LDS_SRGB=0"],
     "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_GRAB=4",
                           "-DYRT_SHADOW_LIGHT_MINOR=16", "-DYRT_XCD_CHUNK_PRIMARY=64",
                           "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0"],

@@ -6,7 +6,8 @@ rule 24: cross-process timings are not comparable).
 
 Each library is loaded with RTLD_LOCAL (own kernels, shared HIP runtime), renders
 the c4 frame (instance10000, 1080p, 8x8 spp) into a device buffer on its own
-stream, and reports per-phase GPU ms (library HIP events) per round.
+stream, and reports per-phase GPU ms (library HIP events) per round, their total, and
+the wall time of the call through the end of its kernels ("wall": host gaps included).
 """
 from __future__ import annotations
 
@@ -17,6 +18,7 @@ import json
 import os
 import statistics
 import sys
+import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -74,8 +76,12 @@ def main():
     digest = {}
     for r in range(a.rounds + 1):  # round 0 = warmup
         for name, lib, N, ds, p, stream in runs:
+            stream.synchronize()
+            t0 = time.perf_counter()
             rc = lib.yrt_render(ds, C.byref(p), C.c_void_p(out.data_ptr()), 1, C.c_void_p(stream.cuda_stream))
             assert rc == 0, lib.yrt_last_error()
+            stream.synchronize()
+            wall = (time.perf_counter() - t0) * 1e3  # the call and its kernels, idle gaps included
             t = N.Timings()
             lib.yrt_last_timings(ds, C.byref(t))
             if r == 0:  # warmup; the image digest shows whether the variants agree bit for bit
@@ -86,6 +92,7 @@ def main():
                 if t.launches[k]:
                     res[name].setdefault(ph, []).append(t.ms[k])
             res[name].setdefault("total", []).append(sum(t.ms))
+            res[name].setdefault("wall", []).append(wall)
     if a.count:
         for name, lib, N, ds, p, stream in runs:
             p.count_work, p.timing = 1, 0

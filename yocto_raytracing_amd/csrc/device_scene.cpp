@@ -669,6 +669,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.nwtop = wtop_records;
     v.wide = ds->wide_ok ? 1 : 0;
     v.nlights = (int)lights.size() / 6;
+    v.ntextures = (int)texinfo.size();
     ds->nlights = v.nlights;
     v.ntnodes = (int)tnodes.size() / 2;
     ds->ntnodes = tnodes.size() / 2;
@@ -734,6 +735,8 @@ void device_scene_destroy(device_scene* ds) {
     ds->timer.destroy();
     if (ds->arena) (void)hipFree(ds->arena);
     if (ds->work) (void)hipFree(ds->work);
+    if (ds->level_count_ev) (void)hipEventDestroy(ds->level_count_ev);
+    if (ds->level_count_host) (void)hipHostFree(ds->level_count_host);
     delete ds;
 }
 

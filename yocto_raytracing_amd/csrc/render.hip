@@ -56,10 +56,10 @@ __device__ vec3f shade_path(const dev_scene_view& S, const dev_render_args& A, r
         vec3f la = amb * kd0;
         vec3f tkd = {1, 1, 1}, tks = {1, 1, 1};
         if (kd_txt >= 0) {
-            tkd = eval_texture<COUNT>(S, kd_txt, sf.uv, L.wc);
+            tkd = eval_texture<COUNT>(S, kd_txt, sf.uv, L.wc, S.srgb);
             la = la * tkd;
         }
-        if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, sf.uv, L.wc);
+        if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, sf.uv, L.wc, S.srgb);
         vec3f c = {0.0f, 0.0f, 0.0f};
         for (int li = 0; li < S.nlights; li++) {
             const f4* lr = S.lights + 6 * li;

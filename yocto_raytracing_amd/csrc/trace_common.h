@@ -385,9 +385,11 @@ __device__ __forceinline__ float spec_pow(float x, float y, vec3f ls) {
 
 // lookup_texture + eval_texture (raytrace.cpp:39-86), srgb always on. fmod(u,1)*w in
 // double equals the f32 product: the fmod is exact and the product of two floats is
-// exact in double, so both round once to the same float.
+// exact in double, so both round once to the same float. `lut`: the 256-entry srgb
+// table (S.srgb, or a copy of it in LDS).
 template <bool COUNT>
-__device__ __forceinline__ vec3f eval_texture(const dev_scene_view& S, int tex, vec2f uv, work_counts& wc) {
+__device__ __forceinline__ vec3f eval_texture(const dev_scene_view& S, int tex, vec2f uv, work_counts& wc,
+                                              const float* lut) {
     int4 ti = ld4(S.texinfo + tex);
     if (COUNT) wc.tex++;
     float w = (float)ti.y, h = (float)ti.z;
@@ -406,7 +408,7 @@ __device__ __forceinline__ vec3f eval_texture(const dev_scene_view& S, int tex, 
         int idx = y * ti.y + x;
         idx = idx < 0 ? 0 : (idx >= npix ? npix - 1 : idx);
         uint32_t p = S.texels[ti.x + idx];
-        return {S.srgb[p & 0xff], S.srgb[(p >> 8) & 0xff], S.srgb[(p >> 16) & 0xff]};
+        return {lut[p & 0xff], lut[(p >> 8) & 0xff], lut[(p >> 16) & 0xff]};
     };
     vec3f cij = texel(i, j) * (1 - wi) * (1 - wj);
     vec3f ci1j = texel(i1, j) * wi * (1 - wj);

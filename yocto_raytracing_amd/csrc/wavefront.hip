@@ -72,14 +72,12 @@ struct wf_buffers {
     // level, so any number of levels is plain indexing (the reference recursion has no cap)
     f4* ray_o_;  // level k >= 1 at (k - 1) * capacity: {o.xyz, parent index}
     f4* ray_d_;  // level k >= 1: {d.xyz, -}
-    f4* rec0_;   // level k < nlevels - 1 at k * capacity: {D.xyz, child index}
-    f4* rec1_;   // {la.xyz, -}
-    f4* rec2_;   // {kr.xyz, -}
+    f4* rec0_;   // level k < nlevels - 1 at k * capacity: {D.xyz, material index}
+    f4* rec1_;   // {la.xyz, -}; kr is the material's, re-read where the fold needs it
     __device__ __forceinline__ f4* ray_o(int k) const { return ray_o_ + (size_t)(k - 1) * capacity; }
     __device__ __forceinline__ f4* ray_d(int k) const { return ray_d_ + (size_t)(k - 1) * capacity; }
     __device__ __forceinline__ f4* rec0(int k) const { return rec0_ + (size_t)k * capacity; }
     __device__ __forceinline__ f4* rec1(int k) const { return rec1_ + (size_t)k * capacity; }
-    __device__ __forceinline__ f4* rec2(int k) const { return rec2_ + (size_t)k * capacity; }
     int* count;             // count[k]: rays at level k (k >= 1), nlevels + 1 entries
     unsigned* queue;        // per-XCD work counters of the persistent shadow kernel: [0, 8)
     int capacity;           // samples per chunk
@@ -482,6 +480,12 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
 #endif
 // OCC4 (scenes with at most four lights): the occlusion bytes are loaded together with the
 // surface, one memory round trip instead of one per light inside the light loop.
+#ifndef YRT_SHADE_LDS_SRGB
+// textured scenes: the srgb table (1 KiB) is copied into LDS per block, so the last
+// link of a texture lookup's chain of dependent loads (material -> texel -> table) is
+// an LDS read
+#define YRT_SHADE_LDS_SRGB 1
+#endif
 template <bool COUNT, bool FUSE, int SB = WF_BLOCK, bool OCC4 = false>
 __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
@@ -489,6 +493,13 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
     const int n = level ? B.count[level] : nsamp_level0;
     __shared__ float4 fused_rad[FUSE ? SB : 1];
     __shared__ int cmp_count[SB / 64], cmp_base[SB / 64];
+    __shared__ float srgb_lds[YRT_SHADE_LDS_SRGB ? 256 : 1];
+    // (a scene without textures never looks the table up: it is not staged)
+    const float* lut = YRT_SHADE_LDS_SRGB ? srgb_lds : S.srgb;
+    if (YRT_SHADE_LDS_SRGB && S.ntextures > 0) {  // uniform over the grid
+        for (int q = (int)threadIdx.x; q < 256; q += SB) srgb_lds[q] = S.srgb[q];
+        __syncthreads();
+    }
     work_counts wc;
     unsigned long long truncated = 0;
     const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
@@ -499,7 +510,8 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
     for (int round = 0; round < nround; round++) {
         const int idx = round * stride + blockIdx.x * SB + threadIdx.x;
         bool spawn = false;
-        vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0}, rec_kr = {0, 0, 0};
+        vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0};
+        int rec_mat = 0;
         if (idx < n) {
             float4 s0 = ld4(B.surf0 + idx);
             uint32_t occ_bits = 0;
@@ -533,10 +545,10 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 vec3f la = amb * kd0;
                 vec3f tkd = {1, 1, 1}, tks = {1, 1, 1};
                 if (kd_txt >= 0) {
-                    tkd = eval_texture<COUNT>(S, kd_txt, uv, wc);
+                    tkd = eval_texture<COUNT>(S, kd_txt, uv, wc, lut);
                     la = la * tkd;
                 }
-                if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, uv, wc);
+                if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, uv, wc, lut);
                 vec3f c = {0.0f, 0.0f, 0.0f};
                 // raytrace.cpp:147 (per light) and :196 (mirror): the same value each time
                 const vec3f v = normalize(ro - p);
@@ -585,7 +597,7 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                     dr = (nrm * 2.0f * dot(nrm, v)) - v;
                     rec_d = c;
                     rec_la = la;
-                    rec_kr = kr;
+                    rec_mat = mat;
                     write_r = false;
                 }
                 if (COUNT) wc.hits++;
@@ -601,8 +613,8 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 int lev = level, node = idx;
                 while (lev > 0) {
                     const int parent = ibits(B.ray_o(lev)[node].w);
-                    const float4 d = ld4(B.rec0(lev - 1) + parent), la = ld4(B.rec1(lev - 1) + parent),
-                                 kr = ld4(B.rec2(lev - 1) + parent);
+                    const float4 d = ld4(B.rec0(lev - 1) + parent), la = ld4(B.rec1(lev - 1) + parent);
+                    const float4 kr = ld4(S.mats + 4 * ibits(d.w) + 2);  // the parent's material kr
                     vec3f cc = {d.x, d.y, d.z};
                     cc = cc + vec3f{col.x * kr.x, col.y * kr.y, col.z * kr.z};
                     cc = cc + xyz(la);
@@ -631,9 +643,8 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
             const int slot = cmp_base[w] + __popcll(mask & ((1ull << lane) - 1));
             B.ray_o(level + 1)[slot] = {p.x, p.y, p.z, __int_as_float(idx)};
             B.ray_d(level + 1)[slot] = {dr.x, dr.y, dr.z, 0};
-            B.rec0(level)[idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(slot)};
+            B.rec0(level)[idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(rec_mat)};
             B.rec1(level)[idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
-            B.rec2(level)[idx] = {rec_kr.x, rec_kr.y, rec_kr.z, 0};
         }
     }
     if (FUSE) {
@@ -711,8 +722,8 @@ size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
     size_t b = align_up(sizeof(int) * (size_t)(nlevels + 1)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
-    // levels >= 1: ray_o, ray_d; levels < last: rec0..2 (one slab each)
-    if (nlevels > 1) b += 5 * align_up((size_t)(nlevels - 1) * 16 * c);
+    // levels >= 1: ray_o, ray_d; levels < last: rec0, rec1 (one slab each)
+    if (nlevels > 1) b += 4 * align_up((size_t)(nlevels - 1) * 16 * c);
     return b;
 }
 
@@ -738,7 +749,6 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
         B.ray_d_ = (f4*)take(slab);
         B.rec0_ = (f4*)take(slab);
         B.rec1_ = (f4*)take(slab);
-        B.rec2_ = (f4*)take(slab);
     }
     B.capacity = cap;
     B.nlevels = nlevels;
@@ -756,7 +766,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     // recursion is unbounded, so the caller's depth is kept as given)
     const int nlevels = ds.reflective ? std::max(A.max_depth, 1) : 1;
     // samples per chunk: a whole frame at c3/c4, 15 chunks at c5. A reflective scene keeps
-    // per-level records for every level (80 B per sample and level). The chunk is halved
+    // per-level records for every level (64 B per sample and level). The chunk is halved
     // until the workspace takes at most half of the free HBM (deep mirror recursions run
     // as more, smaller chunks).
     long long target = ds.reflective ? (1ll << 25) : (1ll << CHUNK_LOG2);
@@ -786,6 +796,14 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         ds.work_bytes = need;
     }
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
+    if (nlevels > 1 && !ds.level_count_host) {
+        hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int), hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+    }
+    if (nlevels > 1 && !ds.level_count_ev) {
+        hipError_t e = hipEventCreateWithFlags(&ds.level_count_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
     phase_timer& T = ds.timer;
     const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
     // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE;
@@ -805,22 +823,20 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
                            dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
         T.end(t, stream);
-        // levels run: a level with no mirror rays ends the chunk's recursion (the host reads
-        // the next level's ray count once per level; the per-level launches it saves cost
-        // more than the read)
+        // levels run: a level with no mirror rays ends the chunk's recursion. The host
+        // reads each level's ray count (written by the previous level's k_shade) without
+        // draining the stream: the level's k_bounce, which takes its count on the device,
+        // is queued first, so the GPU works on it while the count comes back; only a
+        // level that turns out empty costs a launch (one k_bounce of no rays)
         for (int level = 0; level < nlevels; level++) {
-            if (level > 0) {
-                int cnt = 0;
-                hipError_t e = hipMemcpyAsync(&cnt, B.count + level, sizeof(int), hipMemcpyDeviceToHost, stream);
-                if (e == hipSuccess) e = hipStreamSynchronize(stream);
-                if (e != hipSuccess) return e;
-                if (cnt == 0) break;
-            }
             if (level > 0) {
                 t = T.begin(phase_bounce, stream);
                 hipLaunchKernelGGL((k_bounce<COUNT, PACKET, SE>), dim3(stride_grid), dim3(WF_BLOCK), 0, stream, ds.view,
                                    level, B, counters);
                 T.end(t, stream);
+                hipError_t e = hipEventSynchronize(ds.level_count_ev);
+                if (e != hipSuccess) return e;
+                if (*ds.level_count_host == 0) break;
             }
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
@@ -866,6 +882,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             }
 #undef YRT_SHADE_LAUNCH
             T.end(t, stream);
+            if (level + 1 < nlevels) {
+                hipError_t e = hipMemcpyAsync(ds.level_count_host, B.count + level + 1, sizeof(int),
+                                              hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess) e = hipEventRecord(ds.level_count_ev, stream);
+                if (e != hipSuccess) return e;
+            }
         }
         if (!fuse) {
             t = T.begin(phase_accumulate, stream);

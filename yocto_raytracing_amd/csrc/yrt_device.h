@@ -98,6 +98,7 @@ struct dev_scene_view {
     int wide;  // 1: any-hit queries use the 4-wide walk
     int nlights;
     int ntnodes;
+    int ntextures;
 #ifdef YRT_DEBUG_BOUNDS  // diagnostic build: array sizes for the walks' bounds checks
     int nsnodes, nsprims, ninst, nwnodes;
 #endif

@@ -60,6 +60,9 @@ struct device_scene {
     // wavefront workspace (device), grown on demand
     void* work = nullptr;
     size_t work_bytes = 0;
+    // mirror levels: the next level's ray count, copied back behind the level's kernels
+    int* level_count_host = nullptr;  // pinned
+    hipEvent_t level_count_ev = nullptr;
     phase_timer timer;
 };
 
