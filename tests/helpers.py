@@ -23,6 +23,9 @@ SCENE_NAMES = ("basic", "simple", "refl", "instance10000", "lines", "instance1k"
 # the max_depth the GPU renders the mirror corridor with (its deepest path: 37-40 levels;
 # the reference's recursion has no cap)
 MIRROR_DEPTH = 64
+# edge-case scenes (tests/golden/make_edges.py): no lights, every ray a miss, no
+# instances, a point light alone -- scenes/edge_<name>.yrtscene
+EDGE_SCENES = ("unlit", "sky", "empty", "lightsonly")
 OBJ_SCENES = ("basic", "simple", "refl", "instance10000")
 REFERENCE = Path("/root/reference")
 REF_OBJ = {

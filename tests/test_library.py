@@ -9,7 +9,7 @@ import re
 import numpy as np
 import pytest
 
-from helpers import OBJ_SCENES, REF_OBJ, ROOT, SCENE_NAMES, digests, have_reference, scene_path
+from helpers import EDGE_SCENES, OBJ_SCENES, REF_OBJ, ROOT, SCENE_NAMES, digests, have_reference, scene_path
 
 
 @pytest.fixture(scope="module")
@@ -59,7 +59,7 @@ def test_scene_roundtrip_and_reference_digest(yrt, name, tmp_path):
     assert gzip.open(out).read() == gzip.open(p).read()
 
 
-@pytest.mark.parametrize("name", SCENE_NAMES)
+@pytest.mark.parametrize("name", SCENE_NAMES + tuple(f"edge_{e}" for e in EDGE_SCENES))
 def test_bvh_matches_reference(yrt, name, tmp_path):
     s = yrt.load_scene(str(scene_path(name)))
     yrt.build_bvh(s)

@@ -39,6 +39,24 @@ def test_oracle_render_bitexact_vs_reference_fixture(name, res, spp):
     np.testing.assert_array_equal(img.view(np.uint32), ref.view(np.uint32))
 
 
+def _edge_cases():
+    z = np.load(GOLDEN / "ref_render_edges.npz")
+    for key in z.files:
+        name, kind, r, s = key.rsplit("_", 3)
+        if kind == "img":
+            yield name, int(r[1:]), int(s[1:])
+
+
+@pytest.mark.parametrize("name,res,spp", list(_edge_cases()))
+def test_oracle_edge_scenes_vs_reference_fixture(name, res, spp):
+    """no lights, every ray a miss, no instances at all, only a point light; 2x1 and 12x7
+    frames (tests/golden/make_edges.py)"""
+    z = np.load(GOLDEN / "ref_render_edges.npz")
+    img, nrays, trunc = Oracle(str(scene_path(f"edge_{name}"))).render(res, spp)
+    assert nrays == int(z[f"{name}_rays_r{res}_s{spp}"])
+    np.testing.assert_array_equal(img.view(np.uint32), z[f"{name}_img_r{res}_s{spp}"].view(np.uint32))
+
+
 @pytest.mark.parametrize("name", SCENE_NAMES)
 def test_oracle_trace_bitexact_vs_reference_fixture(name):
     z = np.load(GOLDEN / f"ref_rays_{name}.npz")

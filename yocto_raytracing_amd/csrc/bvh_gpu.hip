@@ -400,9 +400,16 @@ void build_bvh_gpu(scene& scn, bool equal_num, int device, float* kernel_ms) {
         const auto& ist = scn.instances[ii];
         ip.push_back(make_prim(bbox_to_world(ist.frame, scn.shapes[ist.shp].bvh.nodes[0].bbox), ii));
     }
-    if (ip.empty()) throw std::invalid_argument("build_bvh on the GPU: scene has no instances");
-    std::vector<bvh_tree> it = build_trees(ip, {{0, (int)ip.size()}}, device, &ms_inst);
-    scn.bvh = std::move(it[0]);
+    if (ip.empty()) {  // no instances: one empty leaf, as make_node on an empty range
+        bvh_tree empty;
+        empty.nodes.assign(1, bvh_node{});
+        empty.nodes[0].bbox = invalid_bbox3f;
+        empty.nodes[0].isleaf = 1;
+        scn.bvh = std::move(empty);
+    } else {
+        std::vector<bvh_tree> it = build_trees(ip, {{0, (int)ip.size()}}, device, &ms_inst);
+        scn.bvh = std::move(it[0]);
+    }
     scn.has_bvh = true;
     if (kernel_ms) *kernel_ms = ms_shapes + ms_inst;
 }
