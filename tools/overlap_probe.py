@@ -2,7 +2,7 @@
 the scene, i.e. two workspaces) raise throughput over one stream? Frames are identical
 work; the image digests of both replicas are printed.
 
-    python tools/overlap_probe.py [--frames 12] [--streams 2]
+    python tools/overlap_probe.py [--frames 12] [--share R/N]
 """
 from __future__ import annotations
 
@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=12)
     ap.add_argument("--scene", default="instance10000")
+    ap.add_argument("--resolution", type=int, default=1080)
+    ap.add_argument("--share", default="0/1", help="R/N: rank R's 8-row bands of an N-rank split (bench.py)")
     a = ap.parse_args()
     import torch
 
@@ -28,9 +30,18 @@ def main():
     torch.cuda.set_device(0)
     scn = yrt.load_scene(str(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.yrtscene"))
     yrt.build_bvh(scn)
-    reps = [scn.upload(0), scn.upload(0)]
-    p = yrt.render_params(0.1, 1080, 8)
+    reps = [yrt.DeviceScene(scn, 0), yrt.DeviceScene(scn, 0)]  # two workspaces (upload() caches one)
+    from yocto_raytracing_amd.shard import BandLayout, render_params_band
+
+    p = yrt.render_params(0.1, a.resolution, 8)
     W, H = reps[0].image_size(p)
+    rank, world = (int(v) for v in a.share.split("/"))
+    layout = BandLayout(H, world, 8)
+    band, local_rows = render_params_band(layout, rank)
+    if world > 1:
+        p.band, p.band_stride, p.band_offset = band
+        p.tile_h = local_rows
+        H = local_rows
     outs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     for k in range(2):  # warm both replicas (workspace allocation)
