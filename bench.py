@@ -57,8 +57,6 @@ N_CU, CLOCK_HZ = 256, 2.4e9
 SALU_PEAK = N_CU * 1.0 * CLOCK_HZ / 1e9   # G wave-instructions/s
 VALU_PEAK = N_CU * 4 * 0.5 * CLOCK_HZ / 1e9
 BAND = 8
-# per-rank camera samples up to which two frames render at once (c4 at N = 8: 16.6 M)
-DUAL_MAX_SAMPLES = 20_000_000
 PHASE_KERNEL = {"primary": "k_primary<false, true, unsigned int>",
                 "shadow": "k_shadow_persist<0>",
                 "shade": "k_shade<false, true, 256, true>",
@@ -359,21 +357,12 @@ def main():
     backend_name = dist.get_backend() if world > 1 else None
     overlap = world > 1 and (backend_name == "nccl" or os.environ.get("YRT_BENCH_OVERLAP") == "1")
     nbuf = 2 if overlap else 1
-    # at small per-rank shares (c4 at N = 8) a second device replica of the scene (its own
-    # workspace) renders every other frame on a second stream, so one frame's kernel tails
-    # overlap the next frame's (tools/overlap_probe.py --share 0/N, ms/frame one stream ->
-    # two: 1/8 of c4 3.78 -> 3.67; 1/4 7.38 -> 7.32; 1/2 14.09 -> 14.49; whole 27.36 -> 28.70)
-    local_samples = local_rows * W * a.samples * a.samples
-    dual_env = os.environ.get("YRT_BENCH_DUAL")
-    dual = overlap and (dual_env == "1" or (dual_env != "0" and local_samples <= DUAL_MAX_SAMPLES))
-    replicas = [ds, yrt.DeviceScene(scn, local)] if dual else [ds]
     shards = [torch.empty((local_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     gathered = [torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
                 for _ in range(nbuf)]
     frames = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     index = torch.as_tensor(layout.gather_index(), device=dev)
     stream = torch.cuda.current_stream(dev)
-    render_streams = [stream, torch.cuda.Stream(dev)] if dual else [stream, stream]
     comm = torch.cuda.Stream(dev) if overlap else None
     rendered = [torch.cuda.Event() for _ in range(nbuf)]
     gathered_ev = [None] * nbuf
@@ -386,11 +375,10 @@ def main():
             if not a.profile_rank:
                 gather_frame(shards[b], layout, index, gathered[b], frames[b])
             return b
-        rs = render_streams[b]  # frame i: replica / stream b when dual (else both are ds / stream)
         if gathered_ev[b] is not None:  # shards[b] is free once its previous gather has read it
-            rs.wait_event(gathered_ev[b])
-        replicas[b % len(replicas)].render_into(params, shards[b].data_ptr(), stream=rs.cuda_stream)
-        rendered[b].record(rs)
+            stream.wait_event(gathered_ev[b])
+        ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
+        rendered[b].record(stream)
         with torch.cuda.stream(comm):
             comm.wait_event(rendered[b])
             gather_frame(shards[b], layout, index, gathered[b], frames[b])
@@ -398,26 +386,21 @@ def main():
             gathered_ev[b].record(comm)
         return b
 
-    nwarm = max(a.warmup, len(replicas))  # every replica allocates its workspace before timing
-    for i in range(nwarm):
+    for i in range(a.warmup):
         step(i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        # HIP events around every kernel launch, on the launch stream (library-side); each
-        # replica's first timed frame resets its timers
-        step(i, timing=1 if i < len(replicas) else 2)
+        # HIP events around every kernel launch, on the launch stream (library-side)
+        step(i, timing=1 if i == 0 else 2)
     torch.cuda.synchronize(dev)  # every stream of the device: renders and gathers
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ds.last_stats()
-    phases = {}  # {phase: (ms over the K steps, launches)}, both replicas when dual
-    for r in replicas:
-        for k, (ms, n) in r.last_timings().items():
-            phases[k] = (phases.get(k, (0.0, 0))[0] + ms, phases.get(k, (0.0, 0))[1] + n)
+    phases = ds.last_timings()  # {phase: (ms over the K steps, launches)}
     dom = max(phases, key=lambda k: phases[k][0])
     dom_ms = phases[dom][0] / a.steps  # per frame
     dom_launches = phases[dom][1] / a.steps
@@ -507,7 +490,7 @@ def main():
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": a.steps,
-            "warmup": nwarm,
+            "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
@@ -517,9 +500,7 @@ def main():
             "config": {"workload": f"{a.scene} {W}x{H} {a.samples}x{a.samples} spp, amb 0.1, one frame per step",
                        "scene": a.scene, "width": W, "height": H, "spp": spp,
                        "parallelism": (f"image bands x{world} + {backend_name} all_gather" +
-                                       (" overlapped with the next frame" if overlap else "") +
-                                       ("; two frames rendering at once (two scene replicas, two streams)"
-                                        if dual else "")) if world > 1
+                                       (" overlapped with the next frame" if overlap else "")) if world > 1
                        else "single GPU",
                        "rays_per_frame": total_rays / a.steps,
                        "camera_samples_per_frame": total_samples / a.steps,

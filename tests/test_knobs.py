@@ -30,12 +30,12 @@ VARIANTS = {
     "YRT_SHADOW_WAVES": ["-DYRT_SHADOW_WAVES=6"],
     "YRT_SHADE_WAVES": ["-DYRT_SHADE_WAVES=5"],
     "YRT_SHADE_LDS_SRGB": ["-DYRT_SHADE_LDS_SRGB=0"],
-    "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_GRAB=4",
+    "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_BLOCK_CHUNK=64",
                           "-DYRT_SHADOW_LIGHT_MINOR=16", "-DYRT_XCD_CHUNK_PRIMARY=64",
                           "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0"],
 }
 # knobs covered by another entry's defines
-COVERED = {"YRT_SHADOW_BLOCK", "YRT_SHADOW_GRAB", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
+COVERED = {"YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
            "YRT_SHADOW_PERSIST_MIN_ITEMS"}
 
 

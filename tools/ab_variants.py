@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--samples", type=int, default=8)
     ap.add_argument("--algorithm", type=int, default=0)
     ap.add_argument("--count", action="store_true", help="also print the work counters of one pass")
+    ap.add_argument("--share", default="0/1", help="R/N: render rank R's 8-row bands of an N-rank split")
     a = ap.parse_args()
     import torch  # device buffer + streams
 
@@ -69,6 +70,13 @@ def main():
         p.resolution, p.samples, p.algorithm, p.timing = a.resolution, a.samples, a.algorithm, 1
         w, h = C.c_int(), C.c_int()
         lib.yrt_image_size(ds, C.byref(p), C.byref(w), C.byref(h))
+        rank, world = (int(v) for v in a.share.split("/"))
+        if world > 1:  # bench.py --profile-rank R/N's bands
+            from yocto_raytracing_amd.shard import BandLayout, render_params_band
+
+            layout = BandLayout(h.value, world, 8)
+            (p.band, p.band_stride, p.band_offset), p.tile_h = render_params_band(layout, rank)
+            h = C.c_int(p.tile_h)
         if out is None:
             out = torch.empty((h.value, w.value, 4), dtype=torch.float32, device="cuda")
         runs.append((Path(path).name, lib, N, ds, p, torch.cuda.Stream()))

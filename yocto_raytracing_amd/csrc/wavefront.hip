@@ -55,8 +55,10 @@ constexpr int shadow_block() { return PACKET ? YRT_SHADOW_BLOCK : WF_BLOCK; }
 #ifndef YRT_SHADOW_WAVES
 #define YRT_SHADOW_WAVES YRT_TRACE_WAVES  // the same for k_shadow
 #endif
-#ifndef YRT_SHADOW_GRAB
-#define YRT_SHADOW_GRAB 8  // k_shadow_persist: queue positions taken per atomic (A/B: 2 / 4 / 8 / 32: +82 / -0.8 / -1.9 / +2.4 %)
+#ifndef YRT_SHADOW_BLOCK_CHUNK
+// k_shadow_persist: queue positions per block chunk (A/B at c4 against per-wave grabs of 8:
+// 8 / 16 / 32 / 64 / 128 / 256 / 512: -2.8 / -2.7 / -2.6 / -2.7 / -2.2 / -1.0 / 0 %)
+#define YRT_SHADOW_BLOCK_CHUNK 16
 #endif
 constexpr int CHUNK_LOG2 = 29;  // samples per chunk, non-reflective scenes (~70 B of HBM each)
 constexpr int TILE = 8;         // pixel tiles of TILE x TILE in the sample enumeration
@@ -363,26 +365,26 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     }
 }
 
-// ---- shadow rays of level 0, persistent: a grid of SP_BLOCK-thread blocks that fills the
-// chip once; every wave walks its own share of the (64-sample
-// block, light) items, so no block launch, block retirement or per-block counter flush
-// happens per item. LDSN > 0: each block first stages the first LDSN 4-wide records --
+// ---- shadow rays, persistent: a grid of SP_BLOCK-thread blocks that fills the chip once;
+// every wave walks its own share of the (64-sample block, light) items, so no block
+// launch, block retirement or per-block counter flush happens per item (level 0 with
+// enough items; the kernel also takes a mirror level's sample count from the device). LDSN > 0: each block first stages the first LDSN 4-wide records --
 // the breadth-first top of the instance tree (device_scene.cpp emit_bfs) -- in LDS, and
 // the walk reads those with ds_read_b128 instead of through the scalar cache (the
 // north_star's "hot node tiles staged in LDS").
 //
 // Item order: item = bx * nlights + light (the light index minor, as k_shadow). The
 // hardware deals workgroup b to XCD b % 8; XCD x takes runs x, x + 8, x + 16, ... of C
-// consecutive items (k_shadow's XCD runs), its waves interleaved over them, so all eight
-// XCDs sweep the image together while each traces neighbouring pixels. Items past the
-// last whole super-run are dealt round-robin to every wave.
+// consecutive items (k_shadow's XCD runs), its blocks taking chunks of them in order, so
+// all eight XCDs sweep the image together while each traces neighbouring pixels. Items
+// past the last whole super-run are dealt round-robin to the XCDs.
 #ifndef YRT_SHADOW_PERSIST_MIN_ITEMS
-// the persistent grid pays a tail (its waves' last batches, ~0.26 ms) that the hardware's
-// block dealing does not, and saves the dealing's per-block cost (~6 % of the walk time
-// since the walks got cheaper); it wins with enough items per wave (A/B, items = 64-sample
-// blocks x lights: 6.2 M (a c4 frame) -6 %; 3.1 M (rank 0 of 2) -3 %; 1.6 M +2 %;
-// 0.8 M (rank 0 of 8) +13 %)
-#define YRT_SHADOW_PERSIST_MIN_ITEMS 2000000
+// the persistent grid saves the hardware dealing's per-block cost and, with block chunks,
+// keeps a CU's waves on neighbouring items; it needs enough items per wave to amortise its
+// start and tail (A/B against k_shadow, items = 64-sample blocks x lights: 6.2 M (a c4
+// frame) -6 % before block chunks, which take another 2.7 % off; 1.55 M (rank 0 of 4) -10 %; 1.04 M (c3's level 0) -9 %; 0.78 M (rank 0 of
+// 8) -9.5 %; 43 K (instance10000 at 720p, 1 spp) +1 %; 29 K (c2) +20 %)
+#define YRT_SHADOW_PERSIST_MIN_ITEMS 262144
 #endif
 #ifndef YRT_SHADOW_LDS_RECORDS
 #define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
@@ -415,32 +417,51 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     const unsigned full = n_items / (8u * C) * (8u * C);     // items in whole super-runs
     const unsigned per_xcd = full / 8u;
     unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays traced by this wave
-    // the waves of an XCD take the positions of its item sequence from one agent-scope
-    // counter (one atomic per batch, issued a batch ahead), which keeps the chip's working
-    // window as tight as the hardware's block dealing does (a fixed interleave, wave j
-    // taking j, j + W, ..., lets the waves drift apart: +21 %). The atomic's result stays
-    // in lane 0's VGPR until the next batch needs it, so its latency hides behind the walks
-    auto issue = [&]() -> unsigned {
-        unsigned v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return v;
-    };
-    // YRT_SHADOW_GRAB consecutive positions per atomic (one counter per XCD serialises:
-    // ~11 M atomics/s per address; taking single positions near the end of the sequence
-    // contends there and loses, A/B: full frame +1.5 %, an eighth of it +11 %)
-    constexpr unsigned G = YRT_SHADOW_GRAB;
-    unsigned qv = issue();           // next batch, lane 0
-    unsigned qb = 0, qleft = 0;      // current batch (uniform)
-    // q: this wave's position in its XCD's item sequence; every bound is wave-uniform,
-    // so the whole wave reaches every walk
+    // The waves of an XCD share one agent-scope counter over its item sequence, which keeps
+    // the chip's working window as tight as the hardware's block dealing does (a fixed
+    // interleave, wave j taking j, j + W, ..., lets the waves drift apart: +21 %). Block
+    // chunks: the block takes CS consecutive positions per atomic and its waves take them
+    // one at a time from an LDS counter, so the waves of a CU trace neighbouring items
+    // together (per-wave grabs of 8 consecutive positions: +2.7 %). Chunk g's base sits
+    // in ring entry g % R behind a tag; the wave taking chunk g's middle slot fetches
+    // chunk g + 1, once every slot of the entry's previous chunk has been read (each taker
+    // reads its base right after taking its slot, before it looks at the item, and slots
+    // are taken in order, so every wait ends)
+    constexpr unsigned CS = YRT_SHADOW_BLOCK_CHUNK, R = 4;
+    static_assert(CS >= 2, "a chunk's middle slot fetches the next chunk");
+    __shared__ unsigned ring_base[R], ring_tag[R], ring_reads[R], ring_taken;
+    if (threadIdx.x < R) {
+        ring_tag[threadIdx.x] = threadIdx.x == 0 ? 0u : ~0u;
+        ring_reads[threadIdx.x] = threadIdx.x == 0 ? 0u : CS;
+    }
+    if (threadIdx.x == 0) {
+        ring_base[0] = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * CS;
+        ring_taken = 0;
+    }
+    __syncthreads();
     for (;;) {
-        if (qleft == 0) {
-            qb = (unsigned)__builtin_amdgcn_readfirstlane((int)qv) * G;
-            qleft = G;
-            qv = issue();
+        unsigned t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(&ring_taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+        const unsigned g = t / CS, o = t % CS;
+        if (o == CS / 2) {  // publish chunk g + 1
+            const unsigned e1 = (g + 1) % R;
+            unsigned nbase = 0;
+            if (lane == 0) nbase = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            nbase = (unsigned)__builtin_amdgcn_readfirstlane((int)nbase) * CS;
+            while (__hip_atomic_load(&ring_reads[e1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != CS)
+                __builtin_amdgcn_s_sleep(1);
+            if (lane == 0) {
+                ring_base[e1] = nbase;
+                __hip_atomic_store(&ring_reads[e1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&ring_tag[e1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
-        qleft--;
-        const unsigned q = qb++;
+        const unsigned e = g % R;
+        while (__hip_atomic_load(&ring_tag[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != g)
+            __builtin_amdgcn_s_sleep(1);
+        const unsigned q = (unsigned)__builtin_amdgcn_readfirstlane((int)ring_base[e]) + o;
+        if (lane == 0) __hip_atomic_fetch_add(&ring_reads[e], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         // runs of C items per XCD, then the tail items past the last whole super-run
         const unsigned it = q < per_xcd ? ((q / C) * 8u + xcd) * C + q % C : full + (q - per_xcd) * 8u + xcd;
         if (it >= n_items) break;
@@ -841,6 +862,8 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 t = T.begin(phase_shadow, stream);
+                // level 0 only: at c3 the mirror levels' compacted samples trace faster with the
+                // hardware's dealing (shadow 1.64 -> 1.72 ms with them persistent)
                 if (!COUNT && PACKET && ds.wide_ok && TB == 64 && level == 0 &&
                     (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS) {
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
