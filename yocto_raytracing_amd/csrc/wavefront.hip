@@ -255,6 +255,74 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     return valid;
 }
 
+// ---- work distribution of the persistent any-hit grid: block chunks ----
+// The waves of an XCD share one agent-scope counter over its item sequence, which keeps
+// the chip's working window as tight as the hardware's block dealing does (a fixed
+// interleave, wave j taking j, j + W, ..., lets the waves drift apart: +21 %). A block
+// takes CS consecutive positions per atomic and its waves take them one at a time from
+// an LDS counter, so the waves of a CU trace neighbouring items together (per-wave grabs
+// of 8 consecutive positions: +2.7 % on the any-hit grid). Chunk g's base sits in ring
+// entry g % R behind a tag; the wave taking chunk g's middle slot fetches chunk g + 1,
+// once every slot of the entry's previous chunk has been read (each taker reads its base
+// right after taking its slot, before it looks at the item, and slots are taken in
+// order, so every wait ends). All atomics are vector (lane 0) or LDS operations.
+struct chunk_ring {
+    static constexpr unsigned R = 4;
+    unsigned base[R], tag[R], reads[R], taken;
+};
+
+template <unsigned CS>
+__device__ __forceinline__ void chunk_ring_init(chunk_ring& ring, unsigned* counter) {
+    static_assert(CS >= 2, "a chunk's middle slot fetches the next chunk");
+    if (threadIdx.x < chunk_ring::R) {
+        ring.tag[threadIdx.x] = threadIdx.x == 0 ? 0u : ~0u;
+        ring.reads[threadIdx.x] = threadIdx.x == 0 ? 0u : CS;
+    }
+    if (threadIdx.x == 0) {
+        ring.base[0] = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * CS;
+        ring.taken = 0;
+    }
+    __syncthreads();
+}
+
+// the calling wave's next position in its XCD's item sequence (wave-uniform)
+template <unsigned CS>
+__device__ __forceinline__ unsigned chunk_ring_next(chunk_ring& ring, unsigned* counter, unsigned lane) {
+    constexpr unsigned R = chunk_ring::R;
+    unsigned t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(&ring.taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+    const unsigned g = t / CS, o = t % CS;
+    if (o == CS / 2) {  // publish chunk g + 1
+        const unsigned e1 = (g + 1) % R;
+        unsigned nbase = 0;
+        if (lane == 0) nbase = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nbase = (unsigned)__builtin_amdgcn_readfirstlane((int)nbase) * CS;
+        while (__hip_atomic_load(&ring.reads[e1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != CS)
+            __builtin_amdgcn_s_sleep(1);
+        if (lane == 0) {
+            ring.base[e1] = nbase;
+            __hip_atomic_store(&ring.reads[e1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&ring.tag[e1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    const unsigned e = g % R;
+    while (__hip_atomic_load(&ring.tag[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != g)
+        __builtin_amdgcn_s_sleep(1);
+    const unsigned q = (unsigned)__builtin_amdgcn_readfirstlane((int)ring.base[e]) + o;
+    if (lane == 0) __hip_atomic_fetch_add(&ring.reads[e], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return q;
+}
+
+// position q of XCD xcd's sequence -> item: runs of RUN consecutive items per XCD (XCD x
+// takes runs x, x + 8, ...), then the items past the last whole super-run round-robin
+template <unsigned RUN>
+__device__ __forceinline__ unsigned xcd_item(unsigned q, unsigned xcd, unsigned n_items) {
+    const unsigned full = n_items / (8u * RUN) * (8u * RUN);
+    const unsigned per_xcd = full / 8u;
+    return q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
+}
+
 template <bool COUNT, bool PACKET, typename SE>
 __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A,
                                                                chunk_args C, wf_buffers B,
@@ -389,6 +457,7 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #ifndef YRT_SHADOW_LDS_RECORDS
 #define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
 #endif
+
 constexpr int SP_BLOCK = 1024;  // threads per persistent shadow block (two blocks per CU at 8 waves/SIMD)
 
 template <int LDSN>
@@ -414,56 +483,14 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     const unsigned n_items = (unsigned)nx * (unsigned)nl;
     const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
-    const unsigned full = n_items / (8u * C) * (8u * C);     // items in whole super-runs
-    const unsigned per_xcd = full / 8u;
     unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays traced by this wave
-    // The waves of an XCD share one agent-scope counter over its item sequence, which keeps
-    // the chip's working window as tight as the hardware's block dealing does (a fixed
-    // interleave, wave j taking j, j + W, ..., lets the waves drift apart: +21 %). Block
-    // chunks: the block takes CS consecutive positions per atomic and its waves take them
-    // one at a time from an LDS counter, so the waves of a CU trace neighbouring items
-    // together (per-wave grabs of 8 consecutive positions: +2.7 %). Chunk g's base sits
-    // in ring entry g % R behind a tag; the wave taking chunk g's middle slot fetches
-    // chunk g + 1, once every slot of the entry's previous chunk has been read (each taker
-    // reads its base right after taking its slot, before it looks at the item, and slots
-    // are taken in order, so every wait ends)
-    constexpr unsigned CS = YRT_SHADOW_BLOCK_CHUNK, R = 4;
-    static_assert(CS >= 2, "a chunk's middle slot fetches the next chunk");
-    __shared__ unsigned ring_base[R], ring_tag[R], ring_reads[R], ring_taken;
-    if (threadIdx.x < R) {
-        ring_tag[threadIdx.x] = threadIdx.x == 0 ? 0u : ~0u;
-        ring_reads[threadIdx.x] = threadIdx.x == 0 ? 0u : CS;
-    }
-    if (threadIdx.x == 0) {
-        ring_base[0] = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * CS;
-        ring_taken = 0;
-    }
-    __syncthreads();
+    // positions from the block's chunk ring (chunk_ring_next), YRT_SHADOW_BLOCK_CHUNK at a time
+    constexpr unsigned CS = YRT_SHADOW_BLOCK_CHUNK;
+    __shared__ chunk_ring ring;
+    chunk_ring_init<CS>(ring, B.queue + xcd);
     for (;;) {
-        unsigned t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(&ring_taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
-        const unsigned g = t / CS, o = t % CS;
-        if (o == CS / 2) {  // publish chunk g + 1
-            const unsigned e1 = (g + 1) % R;
-            unsigned nbase = 0;
-            if (lane == 0) nbase = __hip_atomic_fetch_add(B.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            nbase = (unsigned)__builtin_amdgcn_readfirstlane((int)nbase) * CS;
-            while (__hip_atomic_load(&ring_reads[e1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != CS)
-                __builtin_amdgcn_s_sleep(1);
-            if (lane == 0) {
-                ring_base[e1] = nbase;
-                __hip_atomic_store(&ring_reads[e1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_store(&ring_tag[e1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-        const unsigned e = g % R;
-        while (__hip_atomic_load(&ring_tag[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != g)
-            __builtin_amdgcn_s_sleep(1);
-        const unsigned q = (unsigned)__builtin_amdgcn_readfirstlane((int)ring_base[e]) + o;
-        if (lane == 0) __hip_atomic_fetch_add(&ring_reads[e], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // runs of C items per XCD, then the tail items past the last whole super-run
-        const unsigned it = q < per_xcd ? ((q / C) * 8u + xcd) * C + q % C : full + (q - per_xcd) * 8u + xcd;
+        const unsigned q = chunk_ring_next<CS>(ring, B.queue + xcd, lane);
+        const unsigned it = xcd_item<C>(q, xcd, n_items);
         if (it >= n_items) break;
         const int li = (int)(it % (unsigned)nl);
         const int bx = (int)(it / (unsigned)nl);
