@@ -32,11 +32,12 @@ VARIANTS = {
     "YRT_SHADE_LDS_SRGB": ["-DYRT_SHADE_LDS_SRGB=0"],
     "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_BLOCK_CHUNK=64",
                           "-DYRT_SHADOW_LIGHT_MINOR=16", "-DYRT_XCD_CHUNK_PRIMARY=64",
-                          "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0"],
+                          "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0", "-DYRT_PRIMARY_PERSIST_MIN_ITEMS=0",
+                          "-DYRT_PRIMARY_BLOCK_CHUNK=64"],
 }
 # knobs covered by another entry's defines
 COVERED = {"YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
-           "YRT_SHADOW_PERSIST_MIN_ITEMS"}
+           "YRT_SHADOW_PERSIST_MIN_ITEMS", "YRT_PRIMARY_PERSIST_MIN_ITEMS", "YRT_PRIMARY_BLOCK_CHUNK"}
 
 
 def _knobs_in_sources():

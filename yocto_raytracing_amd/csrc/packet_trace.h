@@ -517,7 +517,8 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
 // lane-index compare, no selects). SALU issue -- one scalar unit per CU shared by
 // its four SIMDs -- is what bounds the closest-hit kernels (SQ_INSTS_SALU per CU
 // against the kernel's cycles), so every scalar instruction on the descent counts.
-template <bool COUNT>
+// BS: threads per block of the calling kernel (one LDS slot per thread for the parked 1/d)
+template <bool COUNT, int BS = packet_block>
 __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
                                              work_counts& wc) {
     static_assert(spine_len == 2, "packet_first walks two-node spine records");
@@ -530,7 +531,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
     // the world inverse direction, parked in LDS for the returns from instance leaves
     // (three ds_read instead of three IEEE divisions; three VGPRs stay free)
-    __shared__ float wi_lds[3][packet_block];
+    __shared__ float wi_lds[3][BS];
     wi_lds[0][threadIdx.x] = ci.x, wi_lds[1][threadIdx.x] = ci.y, wi_lds[2][threadIdx.x] = ci.z;
     float hw1 = 0, hw2 = 0;
     int hslot = -1, hei = -1;

@@ -159,7 +159,7 @@ __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool
 // the two traversal schedules behind one call: PACKET = wave-coherent walk
 // (packet_trace.h, default), otherwise one independent walk per lane
 // (trace_common.h). Both are called in wave-uniform control flow.
-template <bool ANY, bool COUNT, bool PACKET, typename SE>
+template <bool ANY, bool COUNT, bool PACKET, typename SE, int BS = packet_block>
 struct tracer {
     SE* lane_stk;
     __device__ __forceinline__ bool trace(const dev_scene_view& S, const ray3& ray, bool valid, hit_record& hr,
@@ -168,7 +168,7 @@ struct tracer {
             if constexpr (ANY)
                 return packet_any<COUNT>(S, ray, valid, wc);
             else
-                return packet_first<COUNT>(S, ray, valid, hr, wc);
+                return packet_first<COUNT, BS>(S, ray, valid, hr, wc);
         }
         if (!valid) return false;
         if (ANY) return occluded<COUNT, WF_BLOCK>(S, ray, lane_stk, wc);
@@ -223,9 +223,9 @@ __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
 
 // ---- level 0: camera rays + closest hit + surface ----
 // the camera samples idx of one wave: eval_camera, closest hit, surface record
-template <bool COUNT, bool PACKET, typename SE>
+template <bool COUNT, bool PACKET, typename SE, int BS = packet_block>
 __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const dev_render_args& A, const chunk_args& C,
-                                                const wf_buffers& B, tracer<false, COUNT, PACKET, SE>& T, int idx,
+                                                const wf_buffers& B, tracer<false, COUNT, PACKET, SE, BS>& T, int idx,
                                                 work_counts& wc) {
     const int nsamp = C.npix * C.spp;
     bool valid = false;
@@ -335,6 +335,53 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
     const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, idx, wc);
     flush_block<2, BS>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
     if (COUNT) flush_work(counters, wc);
+}
+
+// ---- level 0, persistent: k_primary's work on a grid that fills the chip once (two
+// SP_BLOCK-thread blocks per CU), each wave taking 64-sample items through its block's
+// chunk ring (counters B.queue[8..15]). The render, chunk and buffer arguments are read
+// from LDS copies for each item (a compiler barrier per item), so they are not held in
+// registers across the walk.
+constexpr int SP_BLOCK = 1024;  // threads per persistent block (two blocks per CU at 8 waves/SIMD)
+#ifndef YRT_PRIMARY_PERSIST_MIN_ITEMS
+// A/B against k_primary (items = 64-sample blocks; profiles/r3/ab_primary_persist): 2.07 M
+// (c4) primary 11.55 -> 11.37 ms; instance100k 27.16 -> 27.01; 0.52 M (c3; rank 0 of 4)
+// and 0.26 M (rank 0 of 8) unchanged. (Holding the arguments in registers instead: 62 SGPR
+// and 12 VGPR spills, c4 unchanged.)
+#define YRT_PRIMARY_PERSIST_MIN_ITEMS 1000000
+#endif
+#ifndef YRT_PRIMARY_BLOCK_CHUNK
+#define YRT_PRIMARY_BLOCK_CHUNK 16  // (64: the same)
+#endif
+template <typename SE>
+__global__ __launch_bounds__(SP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(dev_scene_view S, dev_render_args A,
+                                                                                chunk_args C, wf_buffers B,
+                                                                                unsigned long long* counters) {
+    constexpr unsigned CS = YRT_PRIMARY_BLOCK_CHUNK;
+    __shared__ chunk_ring ring;
+    __shared__ dev_render_args A_lds;
+    __shared__ chunk_args C_lds;
+    __shared__ wf_buffers B_lds;
+    if (threadIdx.x == 0) A_lds = A, C_lds = C, B_lds = B;
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned xcd = blockIdx.x % 8u;
+    unsigned* counter = B.queue + 8 + xcd;
+    chunk_ring_init<CS>(ring, counter);  // (its barrier also publishes the copies)
+    tracer<false, false, true, SE, SP_BLOCK> T;
+    T.lane_stk = nullptr;
+    const unsigned n_items = (unsigned)((C.npix * C.spp + 63) / 64);
+    work_counts wc;
+    unsigned valid_n = 0;  // wave-uniform: camera samples of this wave
+    for (;;) {
+        const unsigned q = chunk_ring_next<CS>(ring, counter, lane);
+        const unsigned it = xcd_item<YRT_XCD_CHUNK_PRIMARY>(q, xcd, n_items);
+        if (it >= n_items) break;
+        asm volatile("" ::: "memory");
+        const bool valid = primary_samples<false, true, SE, SP_BLOCK>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc);
+        valid_n += (unsigned)__popcll(ballot(valid));
+    }
+    const unsigned long long mine = lane == 0 ? (unsigned long long)valid_n : 0ull;
+    flush_block<2, SP_BLOCK>(counters, {cnt_rays, cnt_samples}, {mine, mine});
 }
 
 // ---- levels >= 1: closest hit of the compacted mirror rays (grid-stride) ----
@@ -457,8 +504,6 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
 #ifndef YRT_SHADOW_LDS_RECORDS
 #define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
 #endif
-
-constexpr int SP_BLOCK = 1024;  // threads per persistent shadow block (two blocks per CU at 8 waves/SIMD)
 
 template <int LDSN>
 __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(dev_scene_view S, int nsamp,
@@ -868,8 +913,20 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         int t = T.begin(phase_primary, stream);
         constexpr int TB = shadow_block<PACKET>();
         const int tgrid = (nsamp + TB - 1) / TB;
-        hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
-                           dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
+        bool persist = false;
+        if constexpr (!COUNT && PACKET) {
+            persist = ((long long)nsamp + 63) / 64 >= (long long)YRT_PRIMARY_PERSIST_MIN_ITEMS;
+            if (persist) {
+                hipError_t e = hipMemsetAsync(B.queue + 8, 0, 8 * sizeof(unsigned), stream);
+                if (e != hipSuccess) return e;
+                const int nb = ds.num_cus * (YRT_TRACE_WAVES * 4 * 64 / SP_BLOCK);
+                hipLaunchKernelGGL((k_primary_persist<SE>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view, A, C, B,
+                                   counters);
+            }
+        }
+        if (!persist)
+            hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
+                               dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
         T.end(t, stream);
         // levels run: a level with no mirror rays ends the chunk's recursion. The host
         // reads each level's ray count (written by the previous level's k_shade) without
