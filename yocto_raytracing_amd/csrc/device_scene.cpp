@@ -621,6 +621,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_wnodes = ab.add(wnodes.data(), wnodes.size() * sizeof(f4));
     size_t o_winst = ab.add(winst.data(), winst.size() * sizeof(f4));
     size_t o_tpair = ab.add(tpair.data(), tpair.size() * sizeof(f4));
+    size_t o_trel = ab.add(tpair.data(), tpair.size() * sizeof(f4));  // rewritten per render
     size_t o_spair = ab.add(spair.data(), spair.size() * sizeof(f4));
     size_t o_tinst_id = ab.add(tinst_id.data(), tinst_id.size() * sizeof(int));
 
@@ -664,6 +665,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.wnodes = (const f4*)(base + o_wnodes);
     v.winst = (const f4*)(base + o_winst);
     v.tpair = (const f4*)(base + o_tpair);
+    ds->trel = (f4*)(base + o_trel);
     v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);
     v.wtop_root = wtop_root * wide_record_bytes;

@@ -450,7 +450,13 @@ constexpr int packet_block = 256;  // >= threads per block of every kernel that 
 // lanes, node: its first slot, cl: count | leaf_bit). Per spine node: one ballot &
 // mask, one leaf test, one push (v_writelane of the record offset and lane mask). A
 // node no lane passes pops inside the descent (no re-dispatch of the octant copy).
-template <int OCT, bool COUNT>
+//
+// REL: the records' bounds are relative to the rays' common origin (every lane's ray starts
+// at the one point the records were rewritten for, k_relative_records): the box test's
+// (bound - o) is the record itself -- the same fp32 value, computed once per frame instead
+// of once per test -- so the slab test is the three products per plane pair and the
+// reference's min/max chains (x - 0.0f folds to x, bit for bit)
+template <int OCT, bool COUNT, bool REL = false>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
@@ -465,8 +471,9 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
                          : "s"(pb), "s"(uniform(node)));
             rec[0] = rec_of(a, 0), rec[1] = rec_of(a, 1), rec[2] = rec_of(a, 2), rec[3] = rec_of(a, 3);
         }
-        const bool p0 = box_oct<OCT>(co, ci, tmin, tmax, rec[0].x, rec[0].y, rec[0].z, rec[1].x, rec[1].y, rec[1].z);
-        const bool p1 = box_oct<OCT>(co, ci, tmin, tmax, rec[2].x, rec[2].y, rec[2].z, rec[3].x, rec[3].y, rec[3].z);
+        const vec3f bo = REL ? vec3f{0.0f, 0.0f, 0.0f} : co;
+        const bool p0 = box_oct<OCT>(bo, ci, tmin, tmax, rec[0].x, rec[0].y, rec[0].z, rec[1].x, rec[1].y, rec[1].z);
+        const bool p1 = box_oct<OCT>(bo, ci, tmin, tmax, rec[2].x, rec[2].y, rec[2].z, rec[3].x, rec[3].y, rec[3].z);
         if (COUNT && (me & 1)) wc.wnode++;
         if (COUNT && (mask & me)) wc.box++;
         const unsigned long long pm0 = ballot(p0) & mask;
@@ -518,9 +525,11 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
 // its four SIMDs -- is what bounds the closest-hit kernels (SQ_INSTS_SALU per CU
 // against the kernel's cycles), so every scalar instruction on the descent counts.
 // BS: threads per block of the calling kernel (one LDS slot per thread for the parked 1/d)
-template <bool COUNT, int BS = packet_block>
+// trel (REL): the instance-level spine records relative to the origin that every lane's
+// ray shares (the camera's, for primary rays); the instance level is walked on them.
+template <bool COUNT, int BS = packet_block, bool REL = false>
 __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
-                                             work_counts& wc) {
+                                             work_counts& wc, const f4* trel = nullptr) {
     static_assert(spine_len == 2, "packet_first walks two-node spine records");
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
@@ -539,7 +548,8 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     unsigned long long done = 0, inst_mask = 0, mask = live;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
     int node = 0;  // byte offset of the current spine record from pbase
-    const f4* pbase = S.tpair;
+    const f4* const ptop = REL ? trel : S.tpair;
+    const f4* pbase = ptop;
     // the octant of the current level's rays when the whole wave shares it (8: mixed):
     // the descent runs the copy with its slab swaps resolved at compile time (box_oct)
     const int woct = wave_octant(ci, live);
@@ -557,18 +567,33 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                   1, node, sp, level, (int)((pbase - S.spair) / 4), base);
         uint32_t lcl = 0;
         const int floor = level ? base : 0;
-#define YRT_FD(o) \
-    first_descend<o, COUNT>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc, floor, done)
-        switch (oct) {
-            case 0: YRT_FD(0); break;
-            case 1: YRT_FD(1); break;
-            case 2: YRT_FD(2); break;
-            case 3: YRT_FD(3); break;
-            case 4: YRT_FD(4); break;
-            case 5: YRT_FD(5); break;
-            case 6: YRT_FD(6); break;
-            case 7: YRT_FD(7); break;
-            default: YRT_FD(8); break;
+#define YRT_FD(o, R)                                                                                          \
+    first_descend<o, COUNT, R>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc, \
+                               floor, done)
+        if (REL && level == 0) {
+            switch (oct) {
+                case 0: YRT_FD(0, REL); break;
+                case 1: YRT_FD(1, REL); break;
+                case 2: YRT_FD(2, REL); break;
+                case 3: YRT_FD(3, REL); break;
+                case 4: YRT_FD(4, REL); break;
+                case 5: YRT_FD(5, REL); break;
+                case 6: YRT_FD(6, REL); break;
+                case 7: YRT_FD(7, REL); break;
+                default: YRT_FD(8, REL); break;
+            }
+        } else {
+            switch (oct) {
+                case 0: YRT_FD(0, false); break;
+                case 1: YRT_FD(1, false); break;
+                case 2: YRT_FD(2, false); break;
+                case 3: YRT_FD(3, false); break;
+                case 4: YRT_FD(4, false); break;
+                case 5: YRT_FD(5, false); break;
+                case 6: YRT_FD(6, false); break;
+                case 7: YRT_FD(7, false); break;
+                default: YRT_FD(8, false); break;
+            }
         }
 #undef YRT_FD
         const unsigned long long lmask = mask;
@@ -660,7 +685,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     continue;
                 }
                 level = 0;
-                pbase = S.tpair;
+                pbase = ptop;
                 co = wo;
                 cd = wd;
                 ci = {wi_lds[0][threadIdx.x], wi_lds[1][threadIdx.x], wi_lds[2][threadIdx.x]};

@@ -82,6 +82,7 @@ struct wf_buffers {
     __device__ __forceinline__ f4* rec1(int k) const { return rec1_ + (size_t)k * capacity; }
     int* count;             // count[k]: rays at level k (k >= 1), nlevels + 1 entries
     unsigned* queue;        // per-XCD work counters of the persistent shadow kernel: [0, 8)
+    const f4* trel;         // instance-level spine records relative to the camera origin
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
 };
@@ -221,6 +222,10 @@ __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
 #define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (A/B: -1.5 %)
 #endif
 
+#ifndef YRT_PRIMARY_REL
+#define YRT_PRIMARY_REL 1  // camera rays walk the instance level on camera-relative records
+#endif
+
 // ---- level 0: camera rays + closest hit + surface ----
 // the camera samples idx of one wave: eval_camera, closest hit, surface record
 template <bool COUNT, bool PACKET, typename SE, int BS = packet_block>
@@ -243,7 +248,13 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
         }
     }
     hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
-    const bool hit = T.trace(S, ray, valid, hr, wc);
+    // every camera ray starts at the camera origin (camera_ray): the packet walk tests the
+    // instance level on the records relative to it
+    bool hit;
+    if constexpr (PACKET && YRT_PRIMARY_REL)
+        hit = packet_first<COUNT, BS, true>(S, ray, valid, hr, wc, B.trel);
+    else
+        hit = T.trace(S, ray, valid, hr, wc);
     if (valid) {
         surface sf = {};
         if (hit) {
@@ -253,6 +264,17 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
         store_surface(B, idx, hit, sf);
     }
     return valid;
+}
+
+// the instance-level spine records with the camera origin subtracted from every bound, in
+// fp32 as the reference's slab test does it ((bbox.min - ray.o), scene.cpp:373-374): what
+// the primary rays' REL walk reads (packet_first)
+__global__ __launch_bounds__(WF_BLOCK) void k_relative_records(const f4* __restrict__ rec, int n, float ox, float oy,
+                                                              float oz, f4* __restrict__ out) {
+    const int i = blockIdx.x * WF_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const float4 r = ld4(rec + i);
+    out[i] = {r.x - ox, r.y - oy, r.z - oz, r.w};
 }
 
 // ---- work distribution of the persistent any-hit grid: block chunks ----
@@ -889,6 +911,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         ds.work_bytes = need;
     }
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
+    B.trel = ds.trel;
+    if constexpr (PACKET) {
+        const int nrec = (int)ds.ntnodes * 2 * spine_len;
+        hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
+                           ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);
+    }
     if (nlevels > 1 && !ds.level_count_host) {
         hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int), hipHostMallocDefault);
         if (e != hipSuccess) return e;

@@ -55,6 +55,9 @@ struct device_scene {
     bool narrow_stack = true;  // all node indices fit 16-bit stack entries
     bool reflective = false;   // any material with kr > 0 (bounce levels needed)
     bool wide_ok = false;      // the 4-wide any-hit walk's stack fits (else the binary walk)
+    // the instance-level spine records with the camera origin subtracted from every bound
+    // (wavefront.hip k_relative_records, rewritten per render): the primary rays' box tests
+    f4* trel = nullptr;
     int nlights = 0;
     int num_cus = 256;  // compute units of the device (persistent grids)
     // wavefront workspace (device), grown on demand
