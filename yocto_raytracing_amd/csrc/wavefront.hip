@@ -222,6 +222,36 @@ __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
 #define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (A/B: -1.5 %)
 #endif
 
+#ifndef YRT_FAST_NORMALIZE
+#define YRT_FAST_NORMALIZE 1  // shadow-ray setup and shading: normalize / length / ke / r^2 through fast_div.h
+#endif
+
+// normalize(a) and length(a) (yrt_math.h, vmath.h:118-122) with fast_div.h's sqrt_nr and
+// rcp_nr when every active lane's dot(a, a) is in sqrt_nr's range -- then l lies in
+// [2^-48, 2^64), is not 0, and 1/l is normal, where both are bit-identical to sqrtf and
+// 1.0f / l -- else the plain calls. Wave-uniform choice: called in any control flow.
+__device__ __forceinline__ void normalize_len(vec3f a, vec3f& n, float& len) {
+    const float d = dot(a, a);
+    if (YRT_FAST_NORMALIZE && !__ballot(!sqrt_nr_ok(d))) {
+        len = sqrt_nr(d);
+        n = a * rcp_nr(len);
+    } else {
+        len = length(a);
+        n = normalize(a);
+    }
+}
+
+// ke / rr (vec3f / float: three divisions) with fast_div.h's div_nr when every active
+// lane's operands are in its range
+__device__ __forceinline__ vec3f div3(vec3f ke, float rr) {
+    if (YRT_FAST_NORMALIZE &&
+        !__ballot(!(div_nr_ok(ke.x, rr) && div_nr_ok(ke.y, rr) && div_nr_ok(ke.z, rr)))) {
+        const float y = rcp_nr(rr);
+        return {div_nr(ke.x, rr, y), div_nr(ke.y, rr, y), div_nr(ke.z, rr, y)};
+    }
+    return ke / rr;
+}
+
 #ifndef YRT_PRIMARY_REL
 #define YRT_PRIMARY_REL 1  // camera rays walk the instance level on camera-relative records
 #endif
@@ -476,8 +506,9 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
             if (ibits(s0.w) >= 0) {
                 vec3f p = xyz(s0);
                 vec3f tp = transform_point(lf, lp0 - p);
-                vec3f l = normalize(tp);
-                float r = length(tp);
+                vec3f l;
+                float r;
+                normalize_len(tp, l, r);
                 sr = {p, l, 0.01f, r - 0.01f};
                 valid = true;
                 rays++;
@@ -572,8 +603,9 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
             if (ibits(s0.w) >= 0) {
                 vec3f p = xyz(s0);
                 vec3f tp = transform_point(lf, lp0 - p);
-                vec3f l = normalize(tp);
-                float r = length(tp);
+                vec3f l;
+                float r;
+                normalize_len(tp, l, r);
                 sr = {p, l, 0.01f, r - 0.01f};
                 valid = true;
             }
@@ -666,7 +698,9 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 if (ks_txt >= 0) tks = eval_texture<COUNT>(S, ks_txt, uv, wc, lut);
                 vec3f c = {0.0f, 0.0f, 0.0f};
                 // raytrace.cpp:147 (per light) and :196 (mirror): the same value each time
-                const vec3f v = normalize(ro - p);
+                vec3f v;
+                float vlen;
+                normalize_len(ro - p, v, vlen);
                 for (int li = 0; li < S.nlights; li++) {
                     if (OCC4 ? ((occ_bits >> li) & 1u) != 0u : B.occl[(size_t)li * B.capacity + idx] != 0) continue;
                     const f4* lr = S.lights + 6 * li;
@@ -677,14 +711,16 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                     frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
                     vec3f lp0 = xyz(lrec[4]), ke = xyz(lrec[5]);
                     vec3f tp = transform_point(lf, lp0 - p);
-                    vec3f l = normalize(tp);
-                    float r = length(tp);
-                    vec3f h = normalize(v + l);
+                    vec3f l, h;
+                    float r, hlen;
+                    normalize_len(tp, l, r);
+                    normalize_len(v + l, h, hlen);
                     vec3f kd = kd0, ks = ks0;
                     if (kd_txt >= 0) kd = kd * tkd;
                     if (ks_txt >= 0) ks = ks * tks;
-                    vec3f ld = kd * (ke / (r * r));
-                    vec3f ls = ks * (ke / (r * r));
+                    const vec3f ker = div3(ke, r * r);
+                    vec3f ld = kd * ker;
+                    vec3f ls = ks * ker;
                     if (kind == kind_lines) {
                         float prodnl = dot(nrm, l);
                         float prodnh = dot(nrm, h);
