@@ -186,6 +186,15 @@ __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float t
     return (den != 0) & !(w1 < 0 || w1 > 1) & !(w2 < 0.0f || w1 + w2 > 1.0f) & !(t < tmin || t > tmax);
 }
 
+// 1 / d per component (the slab test's invd, scene.cpp:372) as fast_div.h's rcp_nr when
+// every lane of `lanes` has all three components in its range (bit-identical there), else
+// the IEEE divisions
+__device__ __forceinline__ vec3f rcp3(vec3f d, unsigned long long lanes) {
+    if (!(ballot(!(rcp_nr_ok(d.x) && rcp_nr_ok(d.y) && rcp_nr_ok(d.z))) & lanes))
+        return {rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z)};
+    return {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+}
+
 // ---- any hit on the reference's binary BVH ----
 // intersect_any (scene.cpp:489) as a packet walk: the instrumented (COUNT) pass, which
 // counts the reference's own box/instance/primitive tests, and scenes too deep for the
@@ -537,7 +546,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     const vec3f wo = wray.o, wd = wray.d;
     const float tmin = wray.tmin;
     float tmax = wray.tmax;
-    vec3f co = wo, cd = wd, ci = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    vec3f co = wo, cd = wd, ci = rcp3(wd, live);
     // the world inverse direction, parked in LDS for the returns from instance leaves
     // (three ds_read instead of three IEEE divisions; three VGPRs stay free)
     __shared__ float wi_lds[3][BS];
@@ -928,7 +937,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
     const vec3f wo = wray.o, wd = wray.d;
-    const vec3f wi = {1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z};
+    const vec3f wi = rcp3(wd, live);
     const float tmin = wray.tmin, tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = wi;
     int stk_word = 0, stk_mlo = 0, stk_mhi = 0;

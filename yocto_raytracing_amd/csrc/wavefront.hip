@@ -252,6 +252,36 @@ __device__ __forceinline__ vec3f div3(vec3f ke, float rr) {
     return ke / rr;
 }
 
+// camera_ray (trace_common.h, raytrace.cpp:6-37 with the uv of :235-238) with its four
+// divisions and normalize through fast_div.h where every active lane is in range (the
+// same bits); called per lane in divergent code (the checks ballot the active lanes)
+__device__ __forceinline__ ray3 camera_ray_w(const dev_camera& cam, int W, int H, int ns, int i, int j, int ii,
+                                             int jj) {
+    const float fns = (float)ns, fw = (float)W, fh = (float)H;
+    const float a = ii + 0.5f, b = jj + 0.5f;
+    float u, v;
+    if (YRT_FAST_NORMALIZE && !__ballot(!(div_nr_ok(a, fns) && div_nr_ok(b, fns)))) {
+        const float y = rcp_nr(fns);
+        u = i + div_nr(a, fns, y), v = j + div_nr(b, fns, y);
+    } else {
+        u = i + a / fns, v = j + b / fns;
+    }
+    if (YRT_FAST_NORMALIZE && !__ballot(!(div_nr_ok(u, fw) && div_nr_ok(v, fh)))) {
+        u = div_nr(u, fw, rcp_nr(fw)), v = div_nr(v, fh, rcp_nr(fh));
+    } else {
+        u = u / fw, v = v / fh;
+    }
+    vec3f q;
+    q.x = cam.ox + (u - 0.5f) * cam.w * cam.xx + (v - 0.5f) * cam.h * cam.yx - cam.focus * cam.zx;
+    q.y = cam.oy + (u - 0.5f) * cam.w * cam.xy + (v - 0.5f) * cam.h * cam.yy - cam.focus * cam.zy;
+    q.z = cam.oz + (u - 0.5f) * cam.w * cam.xz + (v - 0.5f) * cam.h * cam.yz - cam.focus * cam.zz;
+    const vec3f o = {cam.ox, cam.oy, cam.oz};
+    vec3f d;
+    float len;
+    normalize_len(q - o, d, len);
+    return {o, d, ray_eps, flt_max};
+}
+
 #ifndef YRT_PRIMARY_REL
 #define YRT_PRIMARY_REL 1  // camera rays walk the instance level on camera-relative records
 #endif
@@ -272,7 +302,7 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
         valid = pixel_of(A, C.tiles_x, p, lx, ly, i, j);
         if (valid) {
             const int ns = A.samples;
-            ray = camera_ray(A.cam, A.width, A.height, ns, i, j, q % ns, q / ns);
+            ray = camera_ray_w(A.cam, A.width, A.height, ns, i, j, q % ns, q / ns);
         } else {
             B.surf0[idx] = {0, 0, 0, __int_as_float(-2)};
         }
