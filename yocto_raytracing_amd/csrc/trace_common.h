@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "fast_div.h"
 #include "yrt_device.h"
 #include "yrt_math.h"
 
@@ -423,6 +424,32 @@ struct surface {
     int mat, kind;
 };
 
+#ifndef YRT_FAST_NORMALIZE
+#define YRT_FAST_NORMALIZE 1  // shadow-ray setup and shading: normalize / length / ke / r^2 through fast_div.h
+#endif
+
+// normalize(a) and length(a) (yrt_math.h, vmath.h:118-122) with fast_div.h's sqrt_nr and
+// rcp_nr when every active lane's dot(a, a) is in sqrt_nr's range -- then l lies in
+// [2^-48, 2^64), is not 0, and 1/l is normal, where both are bit-identical to sqrtf and
+// 1.0f / l -- else the plain calls. Wave-uniform choice: called in any control flow.
+__device__ __forceinline__ void normalize_len(vec3f a, vec3f& n, float& len) {
+    const float d = dot(a, a);
+    if (YRT_FAST_NORMALIZE && !__ballot(!sqrt_nr_ok(d))) {
+        len = sqrt_nr(d);
+        n = a * rcp_nr(len);
+    } else {
+        len = length(a);
+        n = normalize(a);
+    }
+}
+
+__device__ __forceinline__ vec3f normalize_w(vec3f a) {
+    vec3f n;
+    float len;
+    normalize_len(a, n, len);
+    return n;
+}
+
 // eval_pos / eval_norm / eval_texcoord (scene.h:159-218) for the hit (slot, ei, ew)
 __device__ __forceinline__ surface eval_surface(const dev_scene_view& S, int slot, int ei, vec4f ew) {
     const f4* ti = S.tinst + 4 * slot;
@@ -441,18 +468,18 @@ __device__ __forceinline__ surface eval_surface(const dev_scene_view& S, int slo
         luv = {0, 0};  // points carry no texcoord: the reference reads an empty vector here
     } else if (sh.y == kind_lines) {
         lp = xyz(ld4(S.vpos + e.x)) * ew.x + xyz(ld4(S.vpos + e.y)) * ew.y;
-        ln = normalize(xyz(ld4(S.vnorm + e.x)) * ew.x + xyz(ld4(S.vnorm + e.y)) * ew.y);
+        ln = normalize_w(xyz(ld4(S.vnorm + e.x)) * ew.x + xyz(ld4(S.vnorm + e.y)) * ew.y);
         f2 t0 = S.vuv[e.x], t1 = S.vuv[e.y];
         luv = vec2f{t0.x, t0.y} * ew.x + vec2f{t1.x, t1.y} * ew.y;
     } else {
         lp = xyz(ld4(S.vpos + e.x)) * ew.x + xyz(ld4(S.vpos + e.y)) * ew.y + xyz(ld4(S.vpos + e.z)) * ew.z;
-        ln = normalize(xyz(ld4(S.vnorm + e.x)) * ew.x + xyz(ld4(S.vnorm + e.y)) * ew.y +
-                       xyz(ld4(S.vnorm + e.z)) * ew.z);
+        ln = normalize_w(xyz(ld4(S.vnorm + e.x)) * ew.x + xyz(ld4(S.vnorm + e.y)) * ew.y +
+                         xyz(ld4(S.vnorm + e.z)) * ew.z);
         f2 t0 = S.vuv[e.x], t1 = S.vuv[e.y], t2 = S.vuv[e.z];
         luv = vec2f{t0.x, t0.y} * ew.x + vec2f{t1.x, t1.y} * ew.y + vec2f{t2.x, t2.y} * ew.z;
     }
     sf.p = transform_point(f, lp);
-    sf.n = transform_direction(f, ln);
+    sf.n = normalize_w(transform_vector(f, ln));  // transform_direction
     sf.uv = luv;
     return sf;
 }

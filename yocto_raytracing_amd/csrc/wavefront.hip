@@ -222,25 +222,6 @@ __device__ __forceinline__ unsigned xcd_runs(unsigned b, unsigned n) {
 #define YRT_XCD_CHUNK_PRIMARY 256  // k_primary: XCD runs of this many blocks (A/B: -1.5 %)
 #endif
 
-#ifndef YRT_FAST_NORMALIZE
-#define YRT_FAST_NORMALIZE 1  // shadow-ray setup and shading: normalize / length / ke / r^2 through fast_div.h
-#endif
-
-// normalize(a) and length(a) (yrt_math.h, vmath.h:118-122) with fast_div.h's sqrt_nr and
-// rcp_nr when every active lane's dot(a, a) is in sqrt_nr's range -- then l lies in
-// [2^-48, 2^64), is not 0, and 1/l is normal, where both are bit-identical to sqrtf and
-// 1.0f / l -- else the plain calls. Wave-uniform choice: called in any control flow.
-__device__ __forceinline__ void normalize_len(vec3f a, vec3f& n, float& len) {
-    const float d = dot(a, a);
-    if (YRT_FAST_NORMALIZE && !__ballot(!sqrt_nr_ok(d))) {
-        len = sqrt_nr(d);
-        n = a * rcp_nr(len);
-    } else {
-        len = length(a);
-        n = normalize(a);
-    }
-}
-
 // ke / rr (vec3f / float: three divisions) with fast_div.h's div_nr when every active
 // lane's operands are in its range
 __device__ __forceinline__ vec3f div3(vec3f ke, float rr) {
@@ -622,9 +603,11 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         if (it >= n_items) break;
         const int li = (int)(it % (unsigned)nl);
         const int bx = (int)(it / (unsigned)nl);
-        const f4* lr = S.lights + 6 * li;
-        const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
-        const vec3f lp0 = xyz(ld4(lr + 4));
+        // the light's frame and position: one wave-uniform record, through the scalar cache
+        float4 lrec[5];
+        ld_records_at<5>(S.lights, (unsigned)(6 * li), lrec);
+        const frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
+        const vec3f lp0 = xyz(lrec[4]);
         const int idx = bx * 64 + (int)lane;
         bool valid = false;
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
