@@ -147,14 +147,24 @@ __device__ __forceinline__ void flush_work(unsigned long long* counters, const w
     flush(counters, cnt_wave_prim_visits, wc.wprim);
 }
 
+// A workspace pointer as a global-memory pointer. k_primary_persist reads its buffer
+// arguments back from an LDS copy, and a pointer loaded from memory is generic to the
+// compiler: its stores would be FLAT, which count against LGKM_CNT as well, so the walk's
+// next s_waitcnt lgkmcnt(0) (every record fetch) would wait for them to reach memory.
+typedef float gvec4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void gstore(f4* p, int idx, float x, float y, float z, float w) {
+    *((__attribute__((address_space(1))) gvec4*)p + idx) = gvec4{x, y, z, w};
+}
+__device__ __forceinline__ void gstore(float* p, int idx, float x) { *((__attribute__((address_space(1))) float*)p + idx) = x; }
+
 __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool hit, const surface& sf) {
     if (!hit) {
-        B.surf0[idx] = {0, 0, 0, __int_as_float(-1)};
+        gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-1));
         return;
     }
-    B.surf0[idx] = {sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind)};
-    B.surf1[idx] = {sf.n.x, sf.n.y, sf.n.z, sf.uv.x};
-    B.surfv[idx] = sf.uv.y;
+    gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind));
+    gstore(B.surf1, idx, sf.n.x, sf.n.y, sf.n.z, sf.uv.x);
+    gstore(B.surfv, idx, sf.uv.y);
 }
 
 // the two traversal schedules behind one call: PACKET = wave-coherent walk
@@ -285,7 +295,7 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
             const int ns = A.samples;
             ray = camera_ray_w(A.cam, A.width, A.height, ns, i, j, q % ns, q / ns);
         } else {
-            B.surf0[idx] = {0, 0, 0, __int_as_float(-2)};
+            gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-2));
         }
     }
     hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
