@@ -32,6 +32,7 @@ VARIANTS = {
     "YRT_SHADE_LDS_SRGB": ["-DYRT_SHADE_LDS_SRGB=0"],
     "YRT_PRIMARY_REL": ["-DYRT_PRIMARY_REL=0"],
     "YRT_FAST_NORMALIZE": ["-DYRT_FAST_NORMALIZE=0"],
+    "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],
     "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_BLOCK_CHUNK=64",
                           "-DYRT_SHADOW_LIGHT_MINOR=16", "-DYRT_XCD_CHUNK_PRIMARY=64",
                           "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0", "-DYRT_PRIMARY_PERSIST_MIN_ITEMS=0",

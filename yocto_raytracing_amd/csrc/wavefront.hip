@@ -80,12 +80,29 @@ struct wf_buffers {
     __device__ __forceinline__ f4* ray_d(int k) const { return ray_d_ + (size_t)(k - 1) * capacity; }
     __device__ __forceinline__ f4* rec0(int k) const { return rec0_ + (size_t)k * capacity; }
     __device__ __forceinline__ f4* rec1(int k) const { return rec1_ + (size_t)k * capacity; }
-    int* count;             // count[k]: rays at level k (k >= 1), nlevels + 1 entries
+    int* count;             // level k >= 1, segment g: rays at count[(k * level_segments + g) * count_stride]
+    int seg;                // slots per segment of a mirror level (seg_count)
     unsigned* queue;        // per-XCD work counters of the persistent shadow kernel: [0, 8)
     const f4* trel;         // instance-level spine records relative to the camera origin
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
 };
+
+// Mirror levels are compacted into level_segments segments of B.seg slots: segment g of
+// level k + 1 holds the mirror rays spawned by k_shade's blocks b with b % 8 == g, at
+// [g * seg, g * seg + count), each segment behind its own counter on its own 128-byte
+// line. (One counter for the whole level serialised k_shade's block atomics: about 7 ns
+// each on one address, ~1 ms of c3's level-0 shading.) Consumers walk the segments in
+// turn, so their waves stay full except for each segment's last one.
+#ifndef YRT_LEVEL_SEGMENTS
+#define YRT_LEVEL_SEGMENTS 8
+#endif
+constexpr int level_segments = YRT_LEVEL_SEGMENTS;  // divides the 2048-block grid of the mirror levels
+static_assert(2048 % level_segments == 0, "segment bound (run()) assumes level_segments | 2048");
+constexpr int count_stride = 32;  // ints: one 128-byte line per counter
+__device__ __forceinline__ int* seg_counter(int* count, int level, int g) {
+    return count + (level * level_segments + g) * count_stride;
+}
 
 struct chunk_args {
     long long pix0;  // first pixel (in tile enumeration order) of this chunk
@@ -463,14 +480,16 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
                                                      unsigned long long* counters) {
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
-    const int n = B.count[level];
     work_counts wc;
     unsigned long long rays = 0;
     const int stride = gridDim.x * WF_BLOCK;
+    for (int g = 0; g < level_segments; g++) {
+    const int n = *seg_counter(B.count, level, g);
     const int nround = (n + stride - 1) / stride;  // uniform: every lane reaches the traversal
     for (int round = 0; round < nround; round++) {
-        const int idx = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
-        const bool valid = idx < n;
+        const int j = round * stride + blockIdx.x * WF_BLOCK + threadIdx.x;
+        const bool valid = j < n;
+        const int idx = g * B.seg + j;
         ray3 ray = {{0, 0, 0}, {0, 0, 1}, ray_eps, flt_max};
         if (valid) {
             float4 o = ld4(B.ray_o(level) + idx), d = ld4(B.ray_d(level) + idx);
@@ -488,6 +507,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
             store_surface(B, idx, hit, sf);
         }
     }
+    }
     flush_block<1>(counters, {cnt_rays}, {rays});
     if (COUNT) flush_work(counters, wc);
 }
@@ -502,7 +522,6 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     constexpr int BS = shadow_block<PACKET>();
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
-    const int n = level ? B.count[level] : nsamp_level0;
     // level 0 (one block per 256 samples and light): the remap runs over the whole
     // (x, light) grid; levels >= 1 are grid-stride and keep their blocks
     // a pixel block's lights in neighbouring blocks (light index minor), dealt in XCD runs
@@ -517,12 +536,15 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     work_counts wc;
     unsigned long long rays = 0;
     const int stride = gridDim.x * BS;
+    for (int g = 0; g < (level ? level_segments : 1); g++) {
+    const int n = level ? *seg_counter(B.count, level, g) : nsamp_level0;
     const int nround = (n + stride - 1) / stride;
     for (int round = 0; round < nround; round++) {
-        const int idx = round * stride + bx * BS + threadIdx.x;
+        const int j = round * stride + bx * BS + threadIdx.x;
+        const int idx = g * B.seg + j;
         bool valid = false;
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
-        if (idx < n) {
+        if (j < n) {
             float4 s0 = ld4(B.surf0 + idx);
             if (ibits(s0.w) >= 0) {
                 vec3f p = xyz(s0);
@@ -542,6 +564,7 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
         else
             occ = T.trace(S, sr, valid, hr, wc);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
+    }
     }
     // shadow rays are counted once, here; yrt_last_stats reports rays = cnt_rays + this
     flush_block<1, BS>(counters, {cnt_shadow_rays}, {rays});
@@ -593,12 +616,6 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         __syncthreads();
     }
     const int nl = S.nlights;
-    // level >= 1 (level passed as -level - 1 in nsamp): the compacted mirror-hit samples,
-    // counted on the device by the level's k_bounce
-    if (nsamp < 0) {
-        nsamp = B.count[-nsamp - 1];
-        nx = (nsamp + 63) / 64;
-    }
     const unsigned n_items = (unsigned)nx * (unsigned)nl;
     const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
@@ -660,7 +677,6 @@ template <bool COUNT, bool FUSE, int SB = WF_BLOCK, bool OCC4 = false>
 __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
-    const int n = level ? B.count[level] : nsamp_level0;
     __shared__ float4 fused_rad[FUSE ? SB : 1];
     __shared__ int cmp_count[SB / 64], cmp_base[SB / 64];
     __shared__ float srgb_lds[YRT_SHADE_LDS_SRGB ? 256 : 1];
@@ -674,15 +690,21 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
     unsigned long long truncated = 0;
     const vec3f amb = {A.amb[0], A.amb[1], A.amb[2]};
     const vec3f cam_o = {A.cam.ox, A.cam.oy, A.cam.oz};
-    // the loop bound is uniform per wave so every lane reaches the ballot below
+    // the loop bounds are uniform per block so every lane reaches the ballot and the
+    // barriers below
     const int stride = gridDim.x * SB;
+    // this block's mirror rays go to segment blockIdx.x % level_segments of the next level
+    const int gout = (int)(blockIdx.x % (unsigned)level_segments);
+    for (int g = 0; g < (level ? level_segments : 1); g++) {
+    const int n = level ? *seg_counter(B.count, level, g) : nsamp_level0;
     const int nround = (n + stride - 1) / stride;
     for (int round = 0; round < nround; round++) {
-        const int idx = round * stride + blockIdx.x * SB + threadIdx.x;
+        const int j = round * stride + blockIdx.x * SB + threadIdx.x;
+        const int idx = g * B.seg + j;
         bool spawn = false;
         vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0};
         int rec_mat = 0;
-        if (idx < n) {
+        if (j < n) {
             float4 s0 = ld4(B.surf0 + idx);
             uint32_t occ_bits = 0;
             if constexpr (OCC4) {
@@ -797,29 +819,32 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 B.rad[node] = {col.x, col.y, col.z, 1.0f};
             }
         }
-        // compaction of the mirror rays: one atomic per BLOCK (a shared counter hit by
-        // every wave serialises); waves take consecutive ranges in wave order, lanes
-        // consecutive slots in lane order (the fold follows parent indices, so the
-        // order is free)
+        // compaction of the mirror rays (the fold follows parent indices, so the order is
+        // free): a sample's own fold records go out at once; the block's mirror rays take
+        // consecutive slots of its segment (waves in wave order, lanes in lane order)
+        // behind one atomic per block. (One atomic per wave: c3 shade 1.99 -> 5.81 ms.)
         if constexpr (FUSE) continue;  // one level: no mirror rays
         const unsigned long long mask = __ballot(spawn);
         const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (spawn) {
+            B.rec0(level)[idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(rec_mat)};
+            B.rec1(level)[idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
+        }
         if (lane == 0) cmp_count[w] = __popcll(mask);
         __syncthreads();
         if (threadIdx.x == 0) {
             int tot = 0;
             for (int q = 0; q < SB / 64; q++) tot += cmp_count[q];
-            int acc = tot ? atomicAdd(B.count + level + 1, tot) : 0;
+            int acc = tot ? atomicAdd(seg_counter(B.count, level + 1, gout), tot) : 0;
             for (int q = 0; q < SB / 64; q++) cmp_base[q] = acc, acc += cmp_count[q];
         }
         __syncthreads();
         if (spawn) {
-            const int slot = cmp_base[w] + __popcll(mask & ((1ull << lane) - 1));
+            const int slot = gout * B.seg + cmp_base[w] + __popcll(mask & ((1ull << lane) - 1));
             B.ray_o(level + 1)[slot] = {p.x, p.y, p.z, __int_as_float(idx)};
             B.ray_d(level + 1)[slot] = {dr.x, dr.y, dr.z, 0};
-            B.rec0(level)[idx] = {rec_d.x, rec_d.y, rec_d.z, __int_as_float(rec_mat)};
-            B.rec1(level)[idx] = {rec_la.x, rec_la.y, rec_la.z, 0};
         }
+    }
     }
     if (FUSE) {
         // raytrace.cpp:232-249: s*s samples of a pixel summed in jj/ii order, then / s*s
@@ -892,9 +917,12 @@ __global__ __launch_bounds__(WF_BLOCK) void k_accumulate(dev_render_args A, chun
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+// the per-level, per-segment mirror-ray counters (seg_counter)
+size_t count_bytes(int nlevels) { return sizeof(int) * (size_t)(nlevels + 1) * level_segments * count_stride; }
+
 size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
-    size_t b = align_up(sizeof(int) * (size_t)(nlevels + 1)) + align_up(16 * sizeof(unsigned));
+    size_t b = align_up(count_bytes(nlevels)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
     // levels >= 1: ray_o, ray_d; levels < last: rec0, rec1 (one slab each)
     if (nlevels > 1) b += 4 * align_up((size_t)(nlevels - 1) * 16 * c);
@@ -910,7 +938,7 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
         p += align_up(bytes);
         return (void*)q;
     };
-    B.count = (int*)take(sizeof(int) * (size_t)(nlevels + 1));
+    B.count = (int*)take(count_bytes(nlevels));
     B.queue = (unsigned*)take(16 * sizeof(unsigned));
     B.surf0 = (f4*)take(16 * c);
     B.surf1 = (f4*)take(16 * c);
@@ -959,7 +987,14 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         while (target > (1ll << 16) && workspace_bytes((int)target, ds.nlights, nlevels) > free_b / 2) target /= 2;
         pix_per_chunk = cap_for(target);
     }
-    const int cap = pix_per_chunk * spp;
+    // slots per sample record: a chunk's samples, and with mirror levels a slack so that
+    // every segment of a level holds whatever k_shade's blocks of that segment spawn: at
+    // level 0 one round of 256-sample blocks puts at most cap / 8 + 256 rays into a
+    // segment, at later levels (a grid-stride grid of 2048 blocks over up to 8 input
+    // segments) at most cap / 8 + 8 * 256
+    const int cap0 = pix_per_chunk * spp;
+    const int seg = cap0 / level_segments + level_segments * WF_BLOCK;
+    const int cap = nlevels > 1 ? level_segments * seg : cap0;
     const size_t need = workspace_bytes(cap, ds.nlights, nlevels);
     if (need > ds.work_bytes) {
         if (ds.work) (void)hipFree(ds.work);
@@ -971,13 +1006,15 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     }
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
     B.trel = ds.trel;
+    B.seg = seg;
     if constexpr (PACKET) {
         const int nrec = (int)ds.ntnodes * 2 * spine_len;
         hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
                            ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);
     }
     if (nlevels > 1 && !ds.level_count_host) {
-        hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int), hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int) * level_segments * count_stride,
+                                     hipHostMallocDefault);
         if (e != hipSuccess) return e;
     }
     if (nlevels > 1 && !ds.level_count_ev) {
@@ -994,7 +1031,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         const int nsamp = C.npix * spp;
         const int grid = (nsamp + WF_BLOCK - 1) / WF_BLOCK;
         if (nlevels > 1) {
-            hipError_t e = hipMemsetAsync(B.count, 0, sizeof(int) * (size_t)(nlevels + 1), stream);
+            hipError_t e = hipMemsetAsync(B.count, 0, count_bytes(nlevels), stream);
             if (e != hipSuccess) return e;
         }
         int t = T.begin(phase_primary, stream);
@@ -1028,7 +1065,9 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 T.end(t, stream);
                 hipError_t e = hipEventSynchronize(ds.level_count_ev);
                 if (e != hipSuccess) return e;
-                if (*ds.level_count_host == 0) break;
+                bool any = false;
+                for (int g = 0; g < level_segments; g++) any |= ds.level_count_host[g * count_stride] != 0;
+                if (!any) break;
             }
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
@@ -1046,10 +1085,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                     constexpr int L = YRT_SHADOW_LDS_RECORDS;
                     if (L > 0 && ds.view.nwtop >= L)
                         hipLaunchKernelGGL((k_shadow_persist<L>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
-                                           level ? -level - 1 : nsamp, tgrid, B, counters);
+                                           nsamp, tgrid, B, counters);
                     else
                         hipLaunchKernelGGL((k_shadow_persist<0>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
-                                           level ? -level - 1 : nsamp, tgrid, B, counters);
+                                           nsamp, tgrid, B, counters);
                 } else if (!COUNT && PACKET && ds.wide_ok)
                     hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), 0,
                                        stream, ds.view, level, nsamp, B, counters);
@@ -1077,8 +1116,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
 #undef YRT_SHADE_LAUNCH
             T.end(t, stream);
             if (level + 1 < nlevels) {
-                hipError_t e = hipMemcpyAsync(ds.level_count_host, B.count + level + 1, sizeof(int),
-                                              hipMemcpyDeviceToHost, stream);
+                hipError_t e = hipMemcpyAsync(ds.level_count_host,
+                                              B.count + (size_t)(level + 1) * level_segments * count_stride,
+                                              sizeof(int) * level_segments * count_stride, hipMemcpyDeviceToHost,
+                                              stream);
                 if (e == hipSuccess) e = hipEventRecord(ds.level_count_ev, stream);
                 if (e != hipSuccess) return e;
             }
