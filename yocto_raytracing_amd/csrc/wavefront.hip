@@ -695,12 +695,14 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
     const int stride = gridDim.x * SB;
     // this block's mirror rays go to segment blockIdx.x % level_segments of the next level
     const int gout = (int)(blockIdx.x % (unsigned)level_segments);
-    for (int g = 0; g < (level ? level_segments : 1); g++) {
-    const int n = level ? *seg_counter(B.count, level, g) : nsamp_level0;
+    // (FUSE runs level 0 only: one segment, no loop)
+    const int nseg = FUSE ? 1 : level ? level_segments : 1;
+    for (int g = 0; g < nseg; g++) {
+    const int n = (!FUSE && level) ? *seg_counter(B.count, level, g) : nsamp_level0;
     const int nround = (n + stride - 1) / stride;
     for (int round = 0; round < nround; round++) {
         const int j = round * stride + blockIdx.x * SB + threadIdx.x;
-        const int idx = g * B.seg + j;
+        const int idx = FUSE ? j : g * B.seg + j;
         bool spawn = false;
         vec3f p = {0, 0, 0}, dr = {0, 0, 0}, rec_d = {0, 0, 0}, rec_la = {0, 0, 0};
         int rec_mat = 0;
