@@ -28,8 +28,10 @@ roofline  the dominant kernel (k_shadow at c4) is bound by instruction ISSUE, no
           CUs at 2.4 GHz). The pipe with the higher fraction is the bound. The HBM
           fraction from the FETCH_SIZE/WRITE_SIZE passes is reported beside it.
 cpu_baseline  the reference itself (oracle/_ref, compiled from the unmodified sources)
-          on a bounded sample of rows of the same frame, single thread; beside it the C
-          restatement (oracle/liboracle.so) on every host core given to this job
+          on a bounded sample of rows of the same frame, single thread, three disjoint
+          row sets (value pooled, spread per set); cpu_baseline_all_cores the reference
+          again on one host thread per core given to this job; cpu_baseline_port_all_cores
+          the C restatement (oracle/liboracle.so, light list precomputed) on those cores
 """
 from __future__ import annotations
 
@@ -134,43 +136,87 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def _timed_rows(run, H: int, budget_s: float, threads: int = 1):
-    """calibrate on the middle row, then time evenly spaced rows filling about
-    `budget_s` of wall time on `threads` threads (at least one row per thread)"""
+def _timed_rows(run, H: int, budget_s: float, threads: int = 1, repeats: int = 1, min_rows: int = 1):
+    """calibrate on the middle row, then time `repeats` disjoint sets of evenly spaced rows
+    (set k offset by k / repeats of the spacing), each filling about budget_s / repeats of
+    wall time on `threads` threads, with at least max(threads, min_rows) rows per set.
+    Returns [(rows, rays, seconds)] per set."""
     t0 = time.perf_counter()
     run(np.array([H // 2], np.int32))
     t1 = time.perf_counter() - t0
-    nrows = max(threads, min(H, int(budget_s * threads / max(t1, 1e-6))))
-    rows = np.linspace(0, H - 1, nrows).astype(np.int32)
-    t0 = time.perf_counter()
-    rays = run(rows)
-    el = time.perf_counter() - t0
-    return rows, rays, el
+    nrows = max(threads, min_rows, min(H // repeats, int(budget_s / repeats * threads / max(t1, 1e-6))))
+    nrows = max(1, min(nrows, H // repeats))
+    step = H / nrows
+    sets = []
+    for k in range(repeats):
+        rows = np.unique(np.minimum(H - 1, (np.arange(nrows) * step + k * step / repeats).astype(np.int32)))
+        t0 = time.perf_counter()
+        rays = run(rows)
+        sets.append((rows, rays, time.perf_counter() - t0))
+    return sets
+
+
+def _baseline_line(sets, W: int, H: int, spp_axis: int, threads: int, kind: str, what: str):
+    """pooled Mrays/s over every timed set (the value), with the per-set spread"""
+    rays = sum(r for _, r, _ in sets)
+    el = sum(t for _, _, t in sets)
+    nrows = sum(len(rows) for rows, _, _ in sets)
+    samples = nrows * W * spp_axis * spp_axis
+    per = [r / t / 1e6 for _, r, t in sets]
+    return {
+        "value": rays / el / 1e6,
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": kind,
+        "repeats": [round(v, 4) for v in per],
+        "min": min(per),
+        "median": float(np.median(per)),
+        "max": max(per),
+        "cpu_model": cpu_model(),
+        "sample": (f"{len(sets)} disjoint sets of evenly spaced rows ({nrows} rows in all) x {W} px x "
+                   f"{spp_axis * spp_axis} spp of the same frame ({samples} camera samples, {rays} rays) in "
+                   f"{el:.1f} s on {threads} thread(s) of {cpu_model()} ({what}); value = all sets pooled, "
+                   f"repeats = each set's own rate; extrapolated full frame {el / samples * W * H * spp_axis ** 2:.0f} s"),
+    }
+
+
+def _reference(scene_file: Path, res: int):
+    """the reference build (oracle/_ref/libyrtref.so) with the scene loaded, or None"""
+    ref_so = ROOT / "oracle" / "_ref" / "libyrtref.so"
+    if not ref_so.exists():
+        return None
+    lib = ctypes.CDLL(str(ref_so))
+    lib.ref_read_scene.restype = ctypes.c_void_p
+    lib.ref_read_scene.argtypes = [ctypes.c_char_p]
+    lib.ref_image_size.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.ref_render_rows_mt.restype = ctypes.c_longlong
+    lib.ref_render_rows_mt.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    scn = lib.ref_read_scene(str(scene_file).encode())
+    w, h = ctypes.c_int(), ctypes.c_int()
+    lib.ref_image_size(scn, res, ctypes.byref(w), ctypes.byref(h))
+    return lib, scn, w.value, h.value
+
+
+def _host_cores() -> int:
+    """the cores this job has: OMP_NUM_THREADS when the host sets it (16 per GPU on the GPU
+    box), else every CPU"""
+    return int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
 
 
 def cpu_baseline(scene_file: Path, res: int, width: int, spp_axis: int, budget_s: float):
-    """The reference's own code (oracle/_ref/libyrtref.so, single thread) on rows of the
-    same frame; the C restatement (1 thread) if the reference build did not travel.
-    Test/baseline infrastructure only."""
-    ref_so = ROOT / "oracle" / "_ref" / "libyrtref.so"
-    if ref_so.exists() and not width:
-        lib = ctypes.CDLL(str(ref_so))
-        lib.ref_read_scene.restype = ctypes.c_void_p
-        lib.ref_read_scene.argtypes = [ctypes.c_char_p]
-        lib.ref_image_size.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-        lib.ref_render_rows.restype = ctypes.c_longlong
-        lib.ref_render_rows.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_int,
-                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
-        scn = lib.ref_read_scene(str(scene_file).encode())
-        w, h = ctypes.c_int(), ctypes.c_int()
-        lib.ref_image_size(scn, res, ctypes.byref(w), ctypes.byref(h))
-        W, H = w.value, h.value
+    """The reference's own code (oracle/_ref/libyrtref.so) on 1 thread: three disjoint sets
+    of at least 16 evenly spaced rows of the same frame; the C restatement (1 thread) if the
+    reference build did not travel. Test/baseline infrastructure only."""
+    ref = None if width else _reference(scene_file, res)
+    if ref is not None:
+        lib, scn, W, H = ref
 
         def run(rows):
             out = np.zeros((len(rows), W, 4), np.float32)
             r = np.ascontiguousarray(rows, np.int32)
-            return lib.ref_render_rows(scn, 0.1, res, spp_axis, r.ctypes.data, len(r), out.ctypes.data)
-        kind = "reference"
+            return lib.ref_render_rows_mt(scn, 0.1, res, spp_axis, r.ctypes.data, len(r), out.ctypes.data, 1)
+        kind, what = "reference", "the reference's eval_camera/shade, oracle/_ref"
     else:
         o = _oracle(scene_file, 1)
         W, H = o.image_size(res)
@@ -178,18 +224,9 @@ def cpu_baseline(scene_file: Path, res: int, width: int, spp_axis: int, budget_s
 
         def run(rows):
             return o.render(res, spp_axis, rows=rows, width=width)[1]
-        kind = "port"
-    rows, rays, el = _timed_rows(run, H, budget_s)
-    samples = len(rows) * W * spp_axis * spp_axis
-    return {
-        "value": rays / el / 1e6,
-        "unit": "Mrays/s",
-        "cores": 1,
-        "kind": kind,
-        "sample": (f"{len(rows)} evenly spaced rows x {W} px x {spp_axis * spp_axis} spp of the same "
-                   f"frame ({samples} camera samples, {rays} rays) in {el:.1f} s on 1 thread of "
-                   f"{cpu_model()}; extrapolated full frame {el / samples * W * H * spp_axis ** 2:.0f} s"),
-    }
+        kind, what = "port", "oracle/oracle.c"
+    sets = _timed_rows(run, H, budget_s, repeats=3, min_rows=16)
+    return _baseline_line(sets, W, H, spp_axis, 1, kind, what)
 
 
 def _oracle(scene_file: Path, threads: int):
@@ -204,27 +241,40 @@ def _oracle(scene_file: Path, threads: int):
 
 
 def cpu_baseline_all_cores(scene_file: Path, res: int, width: int, spp_axis: int, budget_s: float):
-    """The C restatement (oracle.c, OpenMP over rows) on every core this job has:
-    OMP_NUM_THREADS when the host sets it (16 per GPU on the GPU box), else all CPUs."""
-    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    """The reference itself on every core this job has (ref_render_rows_mt: one host thread
+    per core, each running the reference's per-pixel loop body on the next row), three
+    disjoint row sets. None when the reference build did not travel or the frame has an
+    explicit width (the reference cannot express one)."""
+    ref = None if width else _reference(scene_file, res)
+    if ref is None:
+        return None
+    lib, scn, W, H = ref
+    cores = _host_cores()
+
+    def run(rows):
+        out = np.zeros((len(rows), W, 4), np.float32)
+        r = np.ascontiguousarray(rows, np.int32)
+        return lib.ref_render_rows_mt(scn, 0.1, res, spp_axis, r.ctypes.data, len(r), out.ctypes.data, cores)
+    sets = _timed_rows(run, H, budget_s, threads=cores, repeats=3)
+    return _baseline_line(sets, W, H, spp_axis, cores, "reference",
+                          "the reference's eval_camera/shade on one host thread per core, oracle/_ref")
+
+
+def cpu_baseline_port_all_cores(scene_file: Path, res: int, width: int, spp_axis: int, budget_s: float):
+    """The C restatement (oracle.c, OpenMP over rows) on every core this job has. Its light
+    loop visits a precomputed light list instead of scanning all instances as shade() does
+    (raytrace.cpp:121-126), so it is NOT the reference's throughput: a labelled third leg."""
+    cores = _host_cores()
     o = _oracle(scene_file, cores)
     W, H = o.image_size(res)
     W = width or W
 
     def run(rows):
         return o.render(res, spp_axis, rows=rows, width=width)[1]
-    rows, rays, el = _timed_rows(run, H, budget_s, threads=cores)
+    sets = _timed_rows(run, H, budget_s, threads=cores, repeats=3)
     o.lib.oracle_set_threads(1)
-    samples = len(rows) * W * spp_axis * spp_axis
-    return {
-        "value": rays / el / 1e6,
-        "unit": "Mrays/s",
-        "cores": cores,
-        "kind": "port",
-        "sample": (f"{len(rows)} evenly spaced rows x {W} px x {spp_axis * spp_axis} spp ({samples} camera "
-                   f"samples, {rays} rays) in {el:.1f} s on {cores} threads of {cpu_model()} "
-                   f"(oracle/oracle.c, OpenMP over rows)"),
-    }
+    return _baseline_line(sets, W, H, spp_axis, cores, "port",
+                          "oracle/oracle.c, OpenMP over rows, light list precomputed")
 
 
 # ---------------------------------------------------------------- roofline
@@ -530,6 +580,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(scene_file, a.resolution, a.width, a.samples, a.cpu_seconds)
             line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(scene_file, a.resolution, a.width, a.samples,
                                                                     a.cpu_seconds)
+            line["cpu_baseline_port_all_cores"] = cpu_baseline_port_all_cores(scene_file, a.resolution, a.width,
+                                                                              a.samples, a.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

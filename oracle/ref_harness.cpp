@@ -16,7 +16,8 @@
 //
 // Ray counting: shade() (raytrace.o) calls intersect_first/any (scene.o) across
 // object files, so the link step wraps those two symbols (-Wl,--wrap) and the
-// wrappers below count every traced ray of the reference itself.
+// wrappers below count every traced ray of the reference itself, per thread (the
+// all-cores baseline, ref_render_rows_mt, runs shade() on many threads at once).
 #include "scene.h"
 
 #include <zlib.h>
@@ -26,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 // reference functions defined in src/raytrace.cpp (compiled with -Dmain=reference_main)
@@ -34,7 +36,7 @@ vec4f shade(const scene* scn, const std::vector<instance*>& lights, const vec3f&
             const ray3f& ray);
 image4f raytrace(const scene* scn, const vec3f& amb, int resolution, int samples);
 
-static long long g_rays = 0;
+static thread_local long long g_rays = 0;
 
 extern "C" {
 intersection3f __real__Z15intersect_firstPK5sceneRK5ray3f(const scene*, const ray3f&);
@@ -292,6 +294,33 @@ long long ref_render_rows(void* vscn, float amb, int resolution, int samples, co
         }
     }
     return g_rays;
+}
+
+// The same rows rendered by nthreads host threads (the reference's CPU path on all cores,
+// for bench.py's cpu_baseline_all_cores): each thread takes the next row from a shared
+// counter and runs the loop body above on it -- eval_camera and shade() are the
+// reference's, and shade() only reads the scene (its per-call `new`s leak, as in the
+// reference; malloc is thread-safe). Returns the rays traced by all threads.
+long long ref_render_rows_mt(void* vscn, float amb, int resolution, int samples, const int* rows, int nrows,
+                             float* out, int nthreads) {
+    auto scn = (const scene*)vscn;
+    auto cam = scn->cameras.front();
+    const int W = (int)std::round(cam->aspect * resolution);
+    std::atomic<int> next{0};
+    std::atomic<long long> rays{0};
+    auto work = [&]() {
+        long long mine = 0;
+        for (int r; (r = next.fetch_add(1)) < nrows;) {
+            mine += ref_render_rows(vscn, amb, resolution, samples, rows + r, 1, out + (size_t)r * W * 4);
+        }
+        rays += mine;
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthreads; t++) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    (void)cam;
+    return rays.load();
 }
 
 // Per-ray queries. rays: n x 8 floats (o.xyz, d.xyz, tmin, tmax).

@@ -82,3 +82,18 @@ def test_edge_scene_gpu_bvh_build_equals_reference(yrt, name, tmp_path):
     out = tmp_path / "gpu.yrtbvh"
     s.save_bvh(str(out))
     assert hashlib.sha256(gzip.open(out).read()).hexdigest() == digests()[f"edge_{name}"]["bvh_sha256"]
+
+
+def test_upload_refuses_a_shape_mixing_primitive_kinds(yrt, tmp_path):
+    """A group mixing `f` and `l` (test_library.write_mixed_obj) loads as the reference's
+    one mixed shape, but the reference's answer for it is undefined (its traversal tests
+    the line as a triangle, its shading reads the triangle hit as lines[ei], out of range;
+    test_mixed_kind_group_is_the_references_and_its_lines_are_invisible): the upload refuses
+    it with YRT_ERR_UNSUPPORTED and a message, instead of rendering something."""
+    from test_library import write_mixed_obj
+
+    s = yrt.load_scene(str(write_mixed_obj(tmp_path)))
+    yrt.build_bvh(s)
+    with pytest.raises(yrt.YrtError) as e:
+        s.upload(0)
+    assert "mixes primitive types" in str(e.value)

@@ -241,7 +241,7 @@ def test_full_size_c5_properties(yrt):
     literal square frame needs the explicit width, raytrace.cpp:215-216), 16x16 spp on one
     GPU: 4.29 G camera samples in chunks; every sample traces 1 primary ray and every hit
     3 shadow rays (a handful of corner samples miss the floor at this sampling), nothing
-    truncated, all finite, and row segments equal the oracle"""
+    truncated, 128 evenly spaced whole rows and every non-finite pixel equal the oracle"""
     s = host_scene(yrt, "instance10000")
     img, st = yrt.raytrace(s.upload(0), (0.1, 0.1, 0.1), 4096, 16, width=4096, return_stats=True)
     assert img.shape == (4096, 4096, 4)
@@ -252,18 +252,24 @@ def test_full_size_c5_properties(yrt):
     assert (img[..., 3] == 1).all()
     o = Oracle("instance10000")
     # non-finite pixels (a sample whose shading divides by a zero distance or normalises a
-    # zero vector sums to NaN/inf in the reference too): each must be the oracle's
+    # zero vector sums to NaN/inf in the reference too): EVERY one must be the oracle's
     bad = np.argwhere(~np.isfinite(img[..., :3]).all(-1))
     print(f"c5: {len(bad)} non-finite pixels of {4096 * 4096}")
     assert len(bad) < 4096
-    for row, col in bad[:: max(1, len(bad) // 12)][:12]:
-        ref, _, _ = o.render(4096, 16, rows=[row], x0=col, ncols=1, width=4096)
-        assert_same_floats(img[row:row + 1, col:col + 1], ref)
-    for row, x0 in [(0, 0), (1500, 2016), (2048, 4032), (4095, 1000)]:
-        ref, _, _ = o.render(4096, 16, rows=[row], x0=x0, ncols=64, width=4096)
-        seg = img[row:row + 1, x0:x0 + 64]
-        assert close_mask(seg, ref).all(), f"row {row} x0 {x0}"
-        assert np.mean(seg.view(np.uint32) == ref.view(np.uint32)) > 0.99
+    for row in np.unique(bad[:, 0]):
+        cols = bad[bad[:, 0] == row, 1]
+        x0, x1 = int(cols.min()), int(cols.max()) + 1
+        ref, _, _ = o.render(4096, 16, rows=[row], x0=x0, ncols=x1 - x0, width=4096)
+        assert_same_floats(img[row:row + 1, cols], ref[:, cols - x0])
+    # 128 evenly spaced WHOLE rows against the oracle (OpenMP over rows, ~18 s on the box)
+    rows = np.linspace(0, 4095, 128).astype(np.int32)
+    ref, _, trunc = o.render(4096, 16, rows=rows, width=4096)
+    assert trunc == 0
+    seg = img[rows]
+    differ = int(np.sum(seg.view(np.uint32) != ref.view(np.uint32)))
+    print(f"c5 128 rows vs oracle: {differ} of {seg.size} channels not bit-exact")
+    assert close_mask(seg, ref).all()
+    assert np.mean(seg.view(np.uint32) == ref.view(np.uint32)) > 0.99
 
 
 # ---- instance scaling (instance10000's `i`-line pattern, 1 K / 100 K) ----
@@ -273,7 +279,7 @@ def test_instance_scaling_c4_frame(yrt, name, ninst, depth):
     """the scaling scenes at c4's settings (1920x1080, 8x8 spp): every camera sample traces
     one ray and every hit one shadow ray per light, nothing is truncated or overflows, the
     instance BVH depth plus the deepest shape BVH (15) stays within the walks' stack
-    (traversal_stack_cap = 40), and four whole rows equal the oracle"""
+    (traversal_stack_cap = 40), and 64 evenly spaced whole rows equal the oracle"""
     s = host_scene(yrt, name)
     info = s.info()
     assert info["instances"] == ninst and info["bvh_depth"] == depth and info["shape_bvh_depth"] == 15
@@ -283,9 +289,11 @@ def test_instance_scaling_c4_frame(yrt, name, ninst, depth):
     assert st["camera_samples"] == 1920 * 1080 * 64
     assert st["rays"] == st["camera_samples"] + st["shadow_rays"] and st["shadow_rays"] % 3 == 0
     assert st["depth_truncated"] == 0 and st["stack_overflow"] == 0
-    rows = np.array([0, 377, 540, 1079], np.int32)
+    rows = np.linspace(0, 1079, 64).astype(np.int32)
     ref, _, trunc = Oracle(name).render(1080, 8, rows=rows)
     assert trunc == 0
+    differ = int(np.sum(img[rows].view(np.uint32) != ref.view(np.uint32)))
+    print(f"{name} 64 rows vs oracle: {differ} of {img[rows].size} channels not bit-exact")
     assert close_mask(img[rows], ref).all()
     assert np.mean(img[rows].view(np.uint32) == ref.view(np.uint32)) > 0.99
 

@@ -31,6 +31,8 @@ VARIANTS = {
     "YRT_SHADE_WAVES": ["-DYRT_SHADE_WAVES=5"],
     "YRT_SHADE_LDS_SRGB": ["-DYRT_SHADE_LDS_SRGB=0"],
     "YRT_PRIMARY_REL": ["-DYRT_PRIMARY_REL=0"],
+    "YRT_PRIMARY_LDS_RECORDS": ["-DYRT_PRIMARY_LDS_RECORDS=511"],
+    "YRT_PRIMARY_WAVES": ["-DYRT_PRIMARY_WAVES=6", "-DYRT_PRIMARY_SP_BLOCK=768"],
     "YRT_FAST_NORMALIZE": ["-DYRT_FAST_NORMALIZE=0"],
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],
     "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_BLOCK_CHUNK=64",
@@ -39,7 +41,7 @@ VARIANTS = {
                           "-DYRT_PRIMARY_BLOCK_CHUNK=64"],
 }
 # knobs covered by another entry's defines
-COVERED = {"YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
+COVERED = {"YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
            "YRT_SHADOW_PERSIST_MIN_ITEMS", "YRT_PRIMARY_PERSIST_MIN_ITEMS", "YRT_PRIMARY_BLOCK_CHUNK"}
 
 

@@ -122,3 +122,74 @@ def test_save_png_roundtrip(yrt, tmp_path):
         pos += 12 + n
     raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(5, 6 * 4 + 1)
     np.testing.assert_array_equal(raw[:, 1:].reshape(5, 6, 4), yrt.tonemap(img))
+
+
+MIXED_OBJ = """mtllib mix.mtl
+c cam  0  0.785398  1.5  0  5  1 0 0 0 1 0 0 0 1 0.5 0.5 5
+o mixed
+usemtl m0
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+v 5 0 0
+v 5 1 0
+vn 0 0 1
+vt 0 0
+f 1/1/1 2/1/1 3/1/1 4/1/1
+l 5/1/1 6/1/1
+"""
+MIXED_MTL = "newmtl m0\n  Kd 0.5 0.5 0.5\n  Ns 10\n"
+
+
+def write_mixed_obj(d):
+    """one OBJ group holding a quad (`f`, two triangles) and a line (`l`): the reference's
+    loader makes ONE shape with both kinds (yocto_scn.cpp:337-372)"""
+    (d / "mix.mtl").write_text(MIXED_MTL)
+    (d / "mix.obj").write_text(MIXED_OBJ)
+    return d / "mix.obj"
+
+
+@pytest.mark.reference
+@pytest.mark.skipif(not have_reference(), reason="needs /root/reference and oracle/_ref")
+def test_mixed_kind_group_is_the_references_and_its_lines_are_invisible(yrt, tmp_path):
+    """A group that mixes primitive kinds: the product's loader and BVH builder give the
+    reference's bytes (one shape, 2 triangles + 1 line, the line's box in the BVH). The
+    reference's own traversal then treats every leaf primitive of that shape as a triangle
+    (scene.cpp:405-416: `triangles` non-empty wins), so the line is never hit -- its leaf
+    tests triangle 0 -- while eval_pos/eval_norm/eval_texcoord (scene.h:159-206) give lines
+    precedence over triangles, so shading a hit on triangle 1 reads lines[1] of a 1-line
+    shape: out of range, undefined behaviour. The product refuses such a shape at upload
+    (YRT_ERR_UNSUPPORTED, test_gpu_edges.py) and DESIGN.md §9 records why."""
+    import ctypes as C
+
+    obj = write_mixed_obj(tmp_path)
+    lib = C.CDLL(str(ROOT / "oracle/_ref/libyrtref.so"))
+    lib.ref_load_scene.restype = C.c_void_p
+    lib.ref_load_scene.argtypes = [C.c_char_p]
+    lib.ref_write_scene.argtypes = [C.c_void_p, C.c_char_p]
+    lib.ref_write_bvh.argtypes = [C.c_void_p, C.c_char_p]
+    lib.ref_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 5
+    scn = lib.ref_load_scene(str(obj).encode())
+    lib.ref_write_scene(scn, str(tmp_path / "ref.yrtscene").encode())
+    lib.ref_write_bvh(scn, str(tmp_path / "ref.yrtbvh").encode())
+    s = yrt.load_scene(str(obj))
+    info = s.info()
+    assert (info["shapes"], info["triangles"], info["lines"]) == (1, 2, 1)
+    s.save(str(tmp_path / "ours.yrtscene"))
+    yrt.build_bvh(s)
+    s.save_bvh(str(tmp_path / "ours.yrtbvh"))
+    for kind in ("yrtscene", "yrtbvh"):
+        assert gzip.open(tmp_path / f"ours.{kind}").read() == gzip.open(tmp_path / f"ref.{kind}").read(), kind
+    # the reference's queries: a ray at the line alone, one at triangle 1, one at triangle 0
+    rays = np.array([[5, 0.5, 5, 0, 0, -1, 1e-4, 3.4e38], [0.25, 0.75, 5, 0, 0, -1, 1e-4, 3.4e38],
+                     [0.75, 0.25, 5, 0, 0, -1, 1e-4, 3.4e38]], np.float32)
+    n = len(rays)
+    hit, inst, ei = np.zeros(n, np.uint8), np.zeros(n, np.int32), np.zeros(n, np.int32)
+    ew, dist = np.zeros((n, 4), np.float32), np.zeros(n, np.float32)
+    args = [hit.ctypes.data, inst.ctypes.data, ei.ctypes.data, ew.ctypes.data, dist.ctypes.data]
+    lib.ref_trace(scn, rays.ctypes.data, n, 0, *args)
+    assert hit.tolist() == [0, 1, 1] and ei[1:].tolist() == [1, 0]
+    assert ei[1] >= info["lines"]  # shade() would evaluate this triangle hit as lines[1]
+    lib.ref_trace(scn, rays.ctypes.data, n, 1, *args)
+    assert hit.tolist() == [0, 1, 1]

@@ -116,3 +116,31 @@ def test_oracle_trace_degenerate_rays_vs_reference(name):
     assert_same_floats(got["ew"][h], z["ew"][h])
     assert_same_floats(got["dist"][h], z["dist"][h])
     np.testing.assert_array_equal(o.trace(z["rays"], any_hit=True)["hit"], z["any_hit"].astype(bool))
+
+
+@pytest.mark.reference
+@pytest.mark.skipif(not have_reference(), reason="needs /root/reference and oracle/_ref")
+@pytest.mark.parametrize("name,res,spp", [("refl", 40, 2), ("instance10000", 36, 2)])
+def test_reference_all_cores_rows_equal_full_render(name, res, spp):
+    """bench.py's cpu_baseline_all_cores runs the reference's loop body on many host threads
+    (ref_render_rows_mt): its rows and ray count equal the reference's own raytrace()"""
+    lib = C.CDLL(str(ROOT / "oracle/_ref/libyrtref.so"))
+    lib.ref_read_scene.restype = C.c_void_p
+    lib.ref_read_scene.argtypes = [C.c_char_p]
+    lib.ref_image_size.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.ref_render.restype = C.c_longlong
+    lib.ref_render.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_int, C.c_void_p]
+    lib.ref_render_rows_mt.restype = C.c_longlong
+    lib.ref_render_rows_mt.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                       C.c_int]
+    scn = lib.ref_read_scene(str(scene_path(name)).encode())
+    w, h = C.c_int(), C.c_int()
+    lib.ref_image_size(scn, res, C.byref(w), C.byref(h))
+    full = np.zeros((h.value, w.value, 4), np.float32)
+    n_full = lib.ref_render(scn, 0.1, res, spp, full.ctypes.data)
+    rows = np.arange(h.value, dtype=np.int32)
+    for threads in (1, 5):
+        part = np.zeros_like(full)
+        n = lib.ref_render_rows_mt(scn, 0.1, res, spp, rows.ctypes.data, len(rows), part.ctypes.data, threads)
+        assert n == n_full
+        np.testing.assert_array_equal(part.view(np.uint32), full.view(np.uint32))

@@ -501,7 +501,39 @@ device_scene* device_scene_create(const scene& scn, int device) {
         }
         return out;
     };
-    std::vector<f4> tpair = pairs(tnodes, 0, tnodes.size() / 2, 0);
+    // The instance level's records are renumbered breadth first, sibling pairs kept
+    // adjacent (the walks find child start+1's record right after start's): the top levels
+    // of the tree lead the array, so k_primary_persist can stage its first records in LDS
+    // (YRT_PRIMARY_LDS_RECORDS). Only the record numbering changes; the tree, and so the
+    // walk's order of tests, is the reference's.
+    std::vector<f4> tpair;
+    {
+        const size_t nn = tnodes.size() / 2;
+        std::vector<uint32_t> bfs(nn, 0), order;  // old index -> breadth-first index, and back
+        order.reserve(nn);
+        if (nn) order.push_back(0);
+        for (size_t q = 0; q < order.size(); q++) {
+            uint32_t cl, start;
+            memcpy(&cl, &tnodes[2 * order[q] + 1].w, 4);
+            memcpy(&start, &tnodes[2 * order[q]].w, 4);
+            if (cl & leaf_bit) continue;
+            if ((size_t)start + 1 >= nn) throw std::runtime_error("instance BVH child out of range");
+            bfs[start] = (uint32_t)order.size(), order.push_back(start);
+            bfs[start + 1] = (uint32_t)order.size(), order.push_back(start + 1);
+        }
+        if (order.size() != nn) throw std::runtime_error("instance BVH has unreachable nodes");
+        std::vector<f4> renum(tnodes.size());
+        for (size_t n = 0; n < nn; n++) {
+            f4 lo = tnodes[2 * order[n]];
+            const f4 hi = tnodes[2 * order[n] + 1];
+            uint32_t cl, start;
+            memcpy(&cl, &hi.w, 4);
+            memcpy(&start, &lo.w, 4);
+            if (!(cl & leaf_bit)) lo.w = as_float((int)bfs[start]);
+            renum[2 * n] = lo, renum[2 * n + 1] = hi;
+        }
+        tpair = pairs(renum, 0, nn, 0);
+    }
     std::vector<f4> spair;
     for (size_t si = 0; si < scn.shapes.size(); si++) {
         const size_t nb = (size_t)shapes[si].x, nn = scn.shapes[si].bvh.nodes.size();

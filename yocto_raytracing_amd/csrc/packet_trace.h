@@ -465,15 +465,23 @@ constexpr int packet_block = 256;  // >= threads per block of every kernel that 
 // (bound - o) is the record itself -- the same fp32 value, computed once per frame instead
 // of once per test -- so the slab test is the three products per plane pair and the
 // reference's min/max chains (x - 0.0f folds to x, bit for bit)
-template <int OCT, bool COUNT, bool REL = false>
+//
+// LDSN > 0 (REL only): the first LDSN records of pbase are also in `lds` (staged per block by
+// k_primary_persist, YRT_PRIMARY_LDS_RECORDS); a record below that offset is read with
+// ds_read_b128 at a wave-uniform address instead of through the scalar cache
+template <int OCT, bool COUNT, bool REL = false, int LDSN = 0>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
-                                              work_counts& wc, int floor, unsigned long long done) {
+                                              work_counts& wc, int floor, unsigned long long done,
+                                              const float4* lds = nullptr) {
     const f4* pb = sgpr_ptr(pbase);  // once per descent, not per record (the compiler kept pbase in VGPRs)
     for (;;) {
         float4 rec[4];
-        {
+        if (LDSN > 0 && (unsigned)node < (unsigned)(LDSN * spine_record_bytes)) {
+            const float4* p = lds + ((unsigned)uniform(node) >> 4);
+            rec[0] = p[0], rec[1] = p[1], rec[2] = p[2], rec[3] = p[3];
+        } else {
             sgpr16 a;
             asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
                          : "=s"(a)
@@ -536,9 +544,11 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
 // BS: threads per block of the calling kernel (one LDS slot per thread for the parked 1/d)
 // trel (REL): the instance-level spine records relative to the origin that every lane's
 // ray shares (the camera's, for primary rays); the instance level is walked on them.
-template <bool COUNT, int BS = packet_block, bool REL = false>
+// LDSN/lds (REL): the first LDSN records of trel staged in LDS by the caller (first_descend).
+template <bool COUNT, int BS = packet_block, bool REL = false, int LDSN = 0>
 __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
-                                             work_counts& wc, const f4* trel = nullptr) {
+                                             work_counts& wc, const f4* trel = nullptr,
+                                             const float4* lds = nullptr) {
     static_assert(spine_len == 2, "packet_first walks two-node spine records");
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
@@ -577,8 +587,8 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
         uint32_t lcl = 0;
         const int floor = level ? base : 0;
 #define YRT_FD(o, R)                                                                                          \
-    first_descend<o, COUNT, R>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo, stk_mhi, lcl, wc, \
-                               floor, done)
+    first_descend<o, COUNT, R, R ? LDSN : 0>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo,     \
+                                            stk_mhi, lcl, wc, floor, done, lds)
         if (REL && level == 0) {
             switch (oct) {
                 case 0: YRT_FD(0, REL); break;

@@ -296,10 +296,10 @@ __device__ __forceinline__ ray3 camera_ray_w(const dev_camera& cam, int W, int H
 
 // ---- level 0: camera rays + closest hit + surface ----
 // the camera samples idx of one wave: eval_camera, closest hit, surface record
-template <bool COUNT, bool PACKET, typename SE, int BS = packet_block>
+template <bool COUNT, bool PACKET, typename SE, int BS = packet_block, int LDSN = 0>
 __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const dev_render_args& A, const chunk_args& C,
                                                 const wf_buffers& B, tracer<false, COUNT, PACKET, SE, BS>& T, int idx,
-                                                work_counts& wc) {
+                                                work_counts& wc, const float4* lds = nullptr) {
     const int nsamp = C.npix * C.spp;
     bool valid = false;
     ray3 ray = {{0, 0, 0}, {0, 0, 1}, ray_eps, flt_max};
@@ -320,7 +320,7 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     // instance level on the records relative to it
     bool hit;
     if constexpr (PACKET && YRT_PRIMARY_REL)
-        hit = packet_first<COUNT, BS, true>(S, ray, valid, hr, wc, B.trel);
+        hit = packet_first<COUNT, BS, true, LDSN>(S, ray, valid, hr, wc, B.trel, lds);
     else
         hit = T.trace(S, ray, valid, hr, wc);
     if (valid) {
@@ -433,6 +433,20 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
 // from LDS copies for each item (a compiler barrier per item), so they are not held in
 // registers across the walk.
 constexpr int SP_BLOCK = 1024;  // threads per persistent block (two blocks per CU at 8 waves/SIMD)
+#ifndef YRT_PRIMARY_WAVES
+#define YRT_PRIMARY_WAVES YRT_TRACE_WAVES  // k_primary_persist: waves per SIMD (register budget and grid)
+#endif
+#ifndef YRT_PRIMARY_SP_BLOCK
+// k_primary_persist: threads per block, whole blocks filling YRT_PRIMARY_WAVES per SIMD
+#define YRT_PRIMARY_SP_BLOCK \
+    (YRT_PRIMARY_WAVES == 7 ? 448 : YRT_PRIMARY_WAVES == 6 ? 768 : YRT_PRIMARY_WAVES == 5 ? 640 : SP_BLOCK)
+#endif
+static_assert((YRT_PRIMARY_WAVES * 4 * 64) % YRT_PRIMARY_SP_BLOCK == 0, "whole blocks per CU");
+#ifndef YRT_PRIMARY_LDS_RECORDS
+// k_primary_persist: the first records of the camera-relative instance level (breadth first,
+// device_scene.cpp) staged in LDS per block, read by the walk instead of through the scalar cache
+#define YRT_PRIMARY_LDS_RECORDS 0
+#endif
 #ifndef YRT_PRIMARY_PERSIST_MIN_ITEMS
 // A/B against k_primary (items = 64-sample blocks; profiles/r3/ab_primary_persist): 2.07 M
 // (c4) primary 11.55 -> 11.37 ms; instance100k 27.16 -> 27.01; 0.52 M (c3; rank 0 of 4)
@@ -443,21 +457,30 @@ constexpr int SP_BLOCK = 1024;  // threads per persistent block (two blocks per 
 #ifndef YRT_PRIMARY_BLOCK_CHUNK
 #define YRT_PRIMARY_BLOCK_CHUNK 16  // (64: the same)
 #endif
-template <typename SE>
-__global__ __launch_bounds__(SP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(dev_scene_view S, dev_render_args A,
-                                                                                chunk_args C, wf_buffers B,
+template <typename SE, int LDSN>
+__global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_primary_persist(dev_scene_view S,
+                                                                                dev_render_args A, chunk_args C,
+                                                                                wf_buffers B,
                                                                                 unsigned long long* counters) {
     constexpr unsigned CS = YRT_PRIMARY_BLOCK_CHUNK;
+    constexpr int SPB = YRT_PRIMARY_SP_BLOCK;
     __shared__ chunk_ring ring;
     __shared__ dev_render_args A_lds;
     __shared__ chunk_args C_lds;
     __shared__ wf_buffers B_lds;
+    __shared__ float4 lds_rec[LDSN > 0 ? LDSN * spine_record_f4 : 1];
+    if constexpr (LDSN > 0) {
+        // (the instance level may have fewer records: the walk never addresses past them)
+        const int n = min(LDSN, S.ntnodes) * spine_record_f4;
+        const float4* src = reinterpret_cast<const float4*>(B.trel);
+        for (int i = (int)threadIdx.x; i < n; i += SPB) lds_rec[i] = src[i];
+    }
     if (threadIdx.x == 0) A_lds = A, C_lds = C, B_lds = B;
     const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
     unsigned* counter = B.queue + 8 + xcd;
     chunk_ring_init<CS>(ring, counter);  // (its barrier also publishes the copies)
-    tracer<false, false, true, SE, SP_BLOCK> T;
+    tracer<false, false, true, SE, SPB> T;
     T.lane_stk = nullptr;
     const unsigned n_items = (unsigned)((C.npix * C.spp + 63) / 64);
     work_counts wc;
@@ -467,11 +490,12 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_TRACE_WAVES) void k_primary_persist(d
         const unsigned it = xcd_item<YRT_XCD_CHUNK_PRIMARY>(q, xcd, n_items);
         if (it >= n_items) break;
         asm volatile("" ::: "memory");
-        const bool valid = primary_samples<false, true, SE, SP_BLOCK>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc);
+        const bool valid =
+            primary_samples<false, true, SE, SPB, LDSN>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc, lds_rec);
         valid_n += (unsigned)__popcll(ballot(valid));
     }
     const unsigned long long mine = lane == 0 ? (unsigned long long)valid_n : 0ull;
-    flush_block<2, SP_BLOCK>(counters, {cnt_rays, cnt_samples}, {mine, mine});
+    flush_block<2, SPB>(counters, {cnt_rays, cnt_samples}, {mine, mine});
 }
 
 // ---- levels >= 1: closest hit of the compacted mirror rays (grid-stride) ----
@@ -1045,9 +1069,9 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (persist) {
                 hipError_t e = hipMemsetAsync(B.queue + 8, 0, 8 * sizeof(unsigned), stream);
                 if (e != hipSuccess) return e;
-                const int nb = ds.num_cus * (YRT_TRACE_WAVES * 4 * 64 / SP_BLOCK);
-                hipLaunchKernelGGL((k_primary_persist<SE>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view, A, C, B,
-                                   counters);
+                const int nb = ds.num_cus * (YRT_PRIMARY_WAVES * 4 * 64 / YRT_PRIMARY_SP_BLOCK);
+                hipLaunchKernelGGL((k_primary_persist<SE, YRT_PRIMARY_LDS_RECORDS>), dim3(nb),
+                                   dim3(YRT_PRIMARY_SP_BLOCK), 0, stream, ds.view, A, C, B, counters);
             }
         }
         if (!persist)
