@@ -97,3 +97,19 @@ def test_upload_refuses_a_shape_mixing_primitive_kinds(yrt, tmp_path):
     with pytest.raises(yrt.YrtError) as e:
         s.upload(0)
     assert "mixes primitive types" in str(e.value)
+
+
+def test_mirror_depth_beyond_hbm_is_refused(yrt):
+    """max_depth = INT_MAX (a natural 'unbounded'): the mirror levels' records (64 B per
+    sample and level) cannot fit even at the smallest chunk, so the render is refused with
+    YRT_ERR_UNSUPPORTED and the sizes, not hipErrorOutOfMemory; a deep but fitting depth
+    renders, and equals the default depth's frame (in/refl's paths are at most 2 deep)"""
+    s = yrt.load_scene(str(scene_path("refl")))
+    yrt.build_bvh(s)
+    ds = s.upload(0)
+    with pytest.raises(yrt.YrtError) as e:
+        yrt.raytrace(ds, (0.1, 0.1, 0.1), 24, 1, max_depth=2**31 - 1)
+    assert "max_depth" in str(e.value) and "MiB" in str(e.value)
+    deep = yrt.raytrace(ds, (0.1, 0.1, 0.1), 24, 1, max_depth=4096)
+    base = yrt.raytrace(ds, (0.1, 0.1, 0.1), 24, 1)
+    np.testing.assert_array_equal(deep.view(np.uint32), base.view(np.uint32))

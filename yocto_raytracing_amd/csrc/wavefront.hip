@@ -174,6 +174,33 @@ __device__ __forceinline__ void gstore(f4* p, int idx, float x, float y, float z
 }
 __device__ __forceinline__ void gstore(float* p, int idx, float x) { *((__attribute__((address_space(1))) float*)p + idx) = x; }
 
+#ifndef YRT_HIT16
+// 1: the closest-hit kernels write a 16-byte hit record {slot, ei, w1, w2} per sample into
+// surf0 instead of the 36-byte surface {p, mat*4+kind} {n, u} {v}; the shadow setup and
+// k_shade evaluate the surface from it (eval_surface) where they need p, n, uv
+#define YRT_HIT16 0
+#endif
+// the sample's record in surf0: HIT16 {slot (-1 miss, -2 not a sample), ei, w1, w2}, else
+// {p, info (mat*4+kind, -1 miss, -2 not a sample)}; the slot/info field
+__device__ __forceinline__ int sample_state(float4 s0) { return YRT_HIT16 ? ibits(s0.x) : ibits(s0.w); }
+__device__ __forceinline__ void store_not_sample(const wf_buffers& B, int idx) {
+    if (YRT_HIT16)
+        gstore(B.surf0, idx, __int_as_float(-2), 0, 0, 0);
+    else
+        gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-2));
+}
+// a HIT16 record's surface (eval_pos/eval_norm/eval_texcoord, scene.h:159-218); ew.x is
+// rebuilt as packet_first builds it (1 - w1 - w2, the same bits)
+__device__ __forceinline__ surface hit16_surface(const dev_scene_view& S, float4 s0) {
+    return eval_surface(S, ibits(s0.x), ibits(s0.y), vec4f{1 - s0.z - s0.w, s0.z, s0.w, 0});
+}
+__device__ __forceinline__ void store_hit16(const wf_buffers& B, int idx, bool hit, const hit_record& hr) {
+    if (!hit)
+        gstore(B.surf0, idx, __int_as_float(-1), 0, 0, 0);
+    else
+        gstore(B.surf0, idx, __int_as_float(hr.slot), __int_as_float(hr.ei), hr.ew.y, hr.ew.z);
+}
+
 __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool hit, const surface& sf) {
     if (!hit) {
         gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-1));
@@ -312,7 +339,7 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
             const int ns = A.samples;
             ray = camera_ray_w(A.cam, A.width, A.height, ns, i, j, q % ns, q / ns);
         } else {
-            gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-2));
+            store_not_sample(B, idx);
         }
     }
     hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
@@ -324,12 +351,14 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     else
         hit = T.trace(S, ray, valid, hr, wc);
     if (valid) {
-        surface sf = {};
-        if (hit) {
-            sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
-            if (COUNT) wc.hits++;
+        if (COUNT && hit) wc.hits++;
+        if (YRT_HIT16) {
+            store_hit16(B, idx, hit, hr);
+        } else {
+            surface sf = {};
+            if (hit) sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
+            store_surface(B, idx, hit, sf);
         }
-        store_surface(B, idx, hit, sf);
     }
     return valid;
 }
@@ -523,12 +552,14 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
         hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
         const bool hit = T.trace(S, ray, valid, hr, wc);
         if (valid) {
-            surface sf = {};
-            if (hit) {
-                sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
-                if (COUNT) wc.hits++;
+            if (COUNT && hit) wc.hits++;
+            if (YRT_HIT16) {
+                store_hit16(B, idx, hit, hr);
+            } else {
+                surface sf = {};
+                if (hit) sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
+                store_surface(B, idx, hit, sf);
             }
-            store_surface(B, idx, hit, sf);
         }
     }
     }
@@ -570,8 +601,8 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
         if (j < n) {
             float4 s0 = ld4(B.surf0 + idx);
-            if (ibits(s0.w) >= 0) {
-                vec3f p = xyz(s0);
+            if (sample_state(s0) >= 0) {
+                const vec3f p = YRT_HIT16 ? hit16_surface(S, s0).p : xyz(s0);
                 vec3f tp = transform_point(lf, lp0 - p);
                 vec3f l;
                 float r;
@@ -664,8 +695,8 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
         if (idx < nsamp) {
             float4 s0 = ld4(B.surf0 + idx);
-            if (ibits(s0.w) >= 0) {
-                vec3f p = xyz(s0);
+            if (sample_state(s0) >= 0) {
+                const vec3f p = YRT_HIT16 ? hit16_surface(S, s0).p : xyz(s0);
                 vec3f tp = transform_point(lf, lp0 - p);
                 vec3f l;
                 float r;
@@ -696,6 +727,12 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
 // link of a texture lookup's chain of dependent loads (material -> texel -> table) is
 // an LDS read
 #define YRT_SHADE_LDS_SRGB 1
+#endif
+#ifndef YRT_FOLD_PREFETCH
+// mirror levels: the parent's fold records (D, la and its material's kr) are loaded at the
+// top of k_shade, beside the sample's own surface, instead of after the shading, so their
+// latency overlaps the light loop rather than following it
+#define YRT_FOLD_PREFETCH 0
 #endif
 template <bool COUNT, bool FUSE, int SB = WF_BLOCK, bool OCC4 = false>
 __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
@@ -741,16 +778,31 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                     occ_bits |= (q < S.nlights && ob != 0u) ? 1u << q : 0u;
                 }
             }
-            const int info = ibits(s0.w);
+            const int info = sample_state(s0);
             vec3f R = {0, 0, 0};
             bool write_r = info != -2;
+            // level >= 1: this sample's ray record {origin, parent index}; with
+            // YRT_FOLD_PREFETCH the parent's fold records are requested now
+            const float4 ro4 = (!FUSE && level) ? ld4(B.ray_o(level) + idx) : make_float4(cam_o.x, cam_o.y, cam_o.z, 0.0f);
+            float4 pd = {0, 0, 0, 0}, pla = {0, 0, 0, 0}, pkr = {0, 0, 0, 0};
+            if (YRT_FOLD_PREFETCH && !FUSE && level) {
+                const int parent = ibits(ro4.w);
+                pd = ld4(B.rec0(level - 1) + parent), pla = ld4(B.rec1(level - 1) + parent);
+                pkr = ld4(S.mats + 4 * ibits(pd.w) + 2);
+            }
             if (info >= 0) {
-                float4 s1 = ld4(B.surf1 + idx);
-                p = xyz(s0);
-                const vec3f nrm = xyz(s1);
-                const vec2f uv = {s1.w, B.surfv[idx]};
-                const int mat = info >> 2, kind = info & 3;
-                const vec3f ro = level ? xyz(ld4(B.ray_o(level) + idx)) : cam_o;
+                vec3f nrm;
+                vec2f uv;
+                int mat, kind;
+                if (YRT_HIT16) {
+                    const surface sf = hit16_surface(S, s0);
+                    p = sf.p, nrm = sf.n, uv = sf.uv, mat = sf.mat, kind = sf.kind;
+                } else {
+                    const float4 s1 = ld4(B.surf1 + idx);
+                    p = xyz(s0), nrm = xyz(s1), uv = {s1.w, B.surfv[idx]};
+                    mat = info >> 2, kind = info & 3;
+                }
+                const vec3f ro = xyz(ro4);
                 float4 m0, m1, m2, m3;
                 {
                     m0 = ld4(S.mats + 4 * mat), m1 = ld4(S.mats + 4 * mat + 1);
@@ -834,9 +886,11 @@ __global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S,
                 vec3f col = R;
                 int lev = level, node = idx;
                 while (lev > 0) {
-                    const int parent = ibits(B.ray_o(lev)[node].w);
-                    const float4 d = ld4(B.rec0(lev - 1) + parent), la = ld4(B.rec1(lev - 1) + parent);
-                    const float4 kr = ld4(S.mats + 4 * ibits(d.w) + 2);  // the parent's material kr
+                    const bool pre = YRT_FOLD_PREFETCH && lev == level;
+                    const int parent = pre ? ibits(ro4.w) : ibits(B.ray_o(lev)[node].w);
+                    const float4 d = pre ? pd : ld4(B.rec0(lev - 1) + parent);
+                    const float4 la = pre ? pla : ld4(B.rec1(lev - 1) + parent);
+                    const float4 kr = pre ? pkr : ld4(S.mats + 4 * ibits(d.w) + 2);  // the parent's material kr
                     vec3f cc = {d.x, d.y, d.z};
                     cc = cc + vec3f{col.x * kr.x, col.y * kr.y, col.z * kr.z};
                     cc = cc + xyz(la);
@@ -944,7 +998,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_accumulate(dev_render_args A, chun
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // the per-level, per-segment mirror-ray counters (seg_counter)
-size_t count_bytes(int nlevels) { return sizeof(int) * (size_t)(nlevels + 1) * level_segments * count_stride; }
+size_t count_bytes(int nlevels) { return sizeof(int) * ((size_t)nlevels + 1) * level_segments * count_stride; }
 
 size_t workspace_bytes(int cap, int nlights, int nlevels) {
     size_t c = (size_t)cap;
@@ -996,31 +1050,37 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     // samples per chunk: a whole frame at c3/c4, 15 chunks at c5. A reflective scene keeps
     // per-level records for every level (64 B per sample and level). The chunk is halved
     // until the workspace takes at most half of the free HBM (deep mirror recursions run
-    // as more, smaller chunks).
+    // as more, smaller chunks); a depth whose smallest chunk (2^16 samples) still does not
+    // fit is refused.
     long long target = ds.reflective ? (1ll << 25) : (1ll << CHUNK_LOG2);
     auto cap_for = [&](long long tgt) {
         int pix = (int)std::max<long long>(1, std::min<long long>(npix_total, tgt / spp));
         pix = ((pix + TILE * TILE - 1) / (TILE * TILE)) * TILE * TILE;
         return pix;
     };
-    int pix_per_chunk = cap_for(target);
-    // the free-memory query (a driver round trip) only when the workspace must grow: a
-    // steady frame loop reuses the workspace it already has
-    if (workspace_bytes(pix_per_chunk * spp, ds.nlights, nlevels) > ds.work_bytes) {
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-        free_b += ds.work_bytes;  // the current workspace is given back if it is regrown
-        while (target > (1ll << 16) && workspace_bytes((int)target, ds.nlights, nlevels) > free_b / 2) target /= 2;
-        pix_per_chunk = cap_for(target);
-    }
     // slots per sample record: a chunk's samples, and with mirror levels a slack so that
     // every segment of a level holds whatever k_shade's blocks of that segment spawn: at
     // level 0 one round of 256-sample blocks puts at most cap / 8 + 256 rays into a
     // segment, at later levels (a grid-stride grid of 2048 blocks over up to 8 input
     // segments) at most cap / 8 + 8 * 256
-    const int cap0 = pix_per_chunk * spp;
-    const int seg = cap0 / level_segments + level_segments * WF_BLOCK;
-    const int cap = nlevels > 1 ? level_segments * seg : cap0;
+    auto seg_of = [&](int pix) { return pix * spp / level_segments + level_segments * WF_BLOCK; };
+    auto cap_of = [&](int pix) { return nlevels > 1 ? level_segments * seg_of(pix) : pix * spp; };
+    auto bytes_of = [&](long long tgt) { return workspace_bytes(cap_of(cap_for(tgt)), ds.nlights, nlevels); };
+    // the free-memory query (a driver round trip) only when the workspace must grow: a
+    // steady frame loop reuses the workspace it already has
+    if (bytes_of(target) > ds.work_bytes) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        free_b += ds.work_bytes;  // the current workspace is given back if it is regrown
+        while (target > (1ll << 16) && bytes_of(target) > free_b / 2) target /= 2;
+        if (bytes_of(target) > free_b)
+            throw unsupported_error("max_depth " + std::to_string(A.max_depth) + " needs " +
+                                    std::to_string(bytes_of(target) >> 20) + " MiB of mirror-level records for its " +
+                                    "smallest chunk; " + std::to_string(free_b >> 20) + " MiB of HBM are free");
+    }
+    const int pix_per_chunk = cap_for(target);
+    const int seg = seg_of(pix_per_chunk);
+    const int cap = cap_of(pix_per_chunk);
     const size_t need = workspace_bytes(cap, ds.nlights, nlevels);
     if (need > ds.work_bytes) {
         if (ds.work) (void)hipFree(ds.work);
@@ -1033,11 +1093,6 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
     B.trel = ds.trel;
     B.seg = seg;
-    if constexpr (PACKET) {
-        const int nrec = (int)ds.ntnodes * 2 * spine_len;
-        hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
-                           ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);
-    }
     if (nlevels > 1 && !ds.level_count_host) {
         hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int) * level_segments * count_stride,
                                      hipHostMallocDefault);
@@ -1061,6 +1116,13 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             if (e != hipSuccess) return e;
         }
         int t = T.begin(phase_primary, stream);
+        if (PACKET && pix0 == 0) {
+            // the camera-relative instance-level records of this render (timed with the
+            // primary phase, whose walk reads them)
+            const int nrec = (int)ds.ntnodes * 2 * spine_len;
+            hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
+                               ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);
+        }
         constexpr int TB = shadow_block<PACKET>();
         const int tgrid = (nsamp + TB - 1) / TB;
         bool persist = false;
