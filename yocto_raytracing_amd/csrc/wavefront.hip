@@ -734,8 +734,11 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
 // latency overlaps the light loop rather than following it
 #define YRT_FOLD_PREFETCH 0
 #endif
+#ifndef YRT_SHADE_LEVEL_WAVES
+#define YRT_SHADE_LEVEL_WAVES YRT_SHADE_WAVES  // the same for the unfused k_shade (reflective scenes)
+#endif
 template <bool COUNT, bool FUSE, int SB = WF_BLOCK, bool OCC4 = false>
-__global__ __launch_bounds__(SB, YRT_SHADE_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
+__global__ __launch_bounds__(SB, FUSE ? YRT_SHADE_WAVES : YRT_SHADE_LEVEL_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
                                                     int max_depth, wf_buffers B, unsigned long long* counters,
                                                     chunk_args C, float4* __restrict__ out) {
     __shared__ float4 fused_rad[FUSE ? SB : 1];
