@@ -33,7 +33,8 @@ VARIANTS = {
     "YRT_PRIMARY_REL": ["-DYRT_PRIMARY_REL=0"],
     "YRT_FOLD_PREFETCH": ["-DYRT_FOLD_PREFETCH=1"],
     "YRT_HIT16": ["-DYRT_HIT16=1"],
-    "YRT_SHADE_LEVEL_WAVES": ["-DYRT_SHADE_LEVEL_WAVES=6"],
+    "YRT_SKIP_UNUSED_V": ["-DYRT_SKIP_UNUSED_V=0"],
+    "YRT_SHADE_LEVEL_WAVES": ["-DYRT_SHADE_LEVEL_WAVES=7"],
     "YRT_PRIMARY_LDS_RECORDS": ["-DYRT_PRIMARY_LDS_RECORDS=511"],
     "YRT_PRIMARY_WAVES": ["-DYRT_PRIMARY_WAVES=6", "-DYRT_PRIMARY_SP_BLOCK=768"],
     "YRT_FAST_NORMALIZE": ["-DYRT_FAST_NORMALIZE=0"],

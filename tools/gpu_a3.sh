@@ -12,6 +12,8 @@ for l in cur lw6 fp1lw6; do
     --scene refl --resolution 1080 --samples 4 > $OUT/pmc_c3_$l.log 2>&1
   rc=$?; echo "pmc c3 $l rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 done
+timeout -k 10 300 python tools/ab_variants.py --rounds 9 $V/libyrt_cur.so $V/libyrt_sv0.so > $OUT/ab_c4_v.txt 2>&1
+rc=$?; grep -v '^{' $OUT/ab_c4_v.txt | grep -v amdgpu.ids; if [ $rc -ne 0 ]; then exit $rc; fi
 for l in cur h16; do
   for c in FETCH_SIZE WRITE_SIZE; do
     YRT_LIB=$V/libyrt_$l.so timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_c4_${l}_$c -o p -- \

@@ -86,6 +86,7 @@ struct wf_buffers {
     const f4* trel;         // instance-level spine records relative to the camera origin
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
+    int need_v;             // the scene has textures: the surface's v (surfv) is stored and read
 };
 
 // Mirror levels are compacted into level_segments segments of B.seg slots: segment g of
@@ -174,6 +175,9 @@ __device__ __forceinline__ void gstore(f4* p, int idx, float x, float y, float z
 }
 __device__ __forceinline__ void gstore(float* p, int idx, float x) { *((__attribute__((address_space(1))) float*)p + idx) = x; }
 
+#ifndef YRT_SKIP_UNUSED_V
+#define YRT_SKIP_UNUSED_V 1  // a scene without textures neither writes nor reads the surface's v
+#endif
 #ifndef YRT_HIT16
 // 1: the closest-hit kernels write a 16-byte hit record {slot, ei, w1, w2} per sample into
 // surf0 instead of the 36-byte surface {p, mat*4+kind} {n, u} {v}; the shadow setup and
@@ -208,7 +212,8 @@ __device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool
     }
     gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind));
     gstore(B.surf1, idx, sf.n.x, sf.n.y, sf.n.z, sf.uv.x);
-    gstore(B.surfv, idx, sf.uv.y);
+    // uv is read only by texture lookups: a scene without textures never needs it
+    if (!YRT_SKIP_UNUSED_V || B.need_v) gstore(B.surfv, idx, sf.uv.y);
 }
 
 // the two traversal schedules behind one call: PACKET = wave-coherent walk
@@ -735,7 +740,10 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
 #define YRT_FOLD_PREFETCH 0
 #endif
 #ifndef YRT_SHADE_LEVEL_WAVES
-#define YRT_SHADE_LEVEL_WAVES YRT_SHADE_WAVES  // the same for the unfused k_shade (reflective scenes)
+// the same for the unfused k_shade (reflective scenes: per-level shading, mirror-ray
+// compaction, the fold). Its waits are dependent loads (SQ_WAIT_ANY 76 % at 7 waves); more
+// registers per wave shorten them (A/B at c3: shade 1.55 -> 1.35 / 1.34 ms at 6 / 5 waves)
+#define YRT_SHADE_LEVEL_WAVES 5
 #endif
 template <bool COUNT, bool FUSE, int SB = WF_BLOCK, bool OCC4 = false>
 __global__ __launch_bounds__(SB, FUSE ? YRT_SHADE_WAVES : YRT_SHADE_LEVEL_WAVES) void k_shade(dev_scene_view S, dev_render_args A, int level, int nsamp_level0,
@@ -802,7 +810,7 @@ __global__ __launch_bounds__(SB, FUSE ? YRT_SHADE_WAVES : YRT_SHADE_LEVEL_WAVES)
                     p = sf.p, nrm = sf.n, uv = sf.uv, mat = sf.mat, kind = sf.kind;
                 } else {
                     const float4 s1 = ld4(B.surf1 + idx);
-                    p = xyz(s0), nrm = xyz(s1), uv = {s1.w, B.surfv[idx]};
+                    p = xyz(s0), nrm = xyz(s1), uv = {s1.w, (!YRT_SKIP_UNUSED_V || B.need_v) ? B.surfv[idx] : 0.0f};
                     mat = info >> 2, kind = info & 3;
                 }
                 const vec3f ro = xyz(ro4);
@@ -1096,6 +1104,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
     B.trel = ds.trel;
     B.seg = seg;
+    B.need_v = ds.view.ntextures > 0;
     if (nlevels > 1 && !ds.level_count_host) {
         hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int) * level_segments * count_stride,
                                      hipHostMallocDefault);
