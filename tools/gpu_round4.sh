@@ -25,7 +25,7 @@ pmc() {  # tag-suffix, timeout, bench args...
   PMC_TIMEOUT=$tmo run bash tools/gpu_issue_pmc.sh $TAG/$sub "$@" > $OUT/$sub.log 2>&1
 }
 if [ "$PART" = A ]; then
-  run timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+  run timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
   tail -n 2 $OUT/pytest.log
   run timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   pmc pmc_c4 150
