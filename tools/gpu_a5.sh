@@ -1,0 +1,14 @@
+set -u
+OUT=gpurun_out/a5
+mkdir -p $OUT
+V=yocto_raytracing_amd/variants
+timeout -k 10 200 python tools/ab_variants.py --rounds 7 $V/libyrt_base.so $V/libyrt_nobun.so $V/libyrt_bun.so > $OUT/ab_c4.txt 2>&1
+rc=$?; grep -v '^{' $OUT/ab_c4.txt | grep -v amdgpu.ids; if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; tail -n 3 $OUT/pytest.log; if [ $rc -ne 0 ]; then exit $rc; fi
+for s in instance100k instance1k; do
+timeout -k 10 200 python tools/ab_variants.py --rounds 5 --scene $s $V/libyrt_nobun.so $V/libyrt_bun.so > $OUT/ab_$s.txt 2>&1
+rc=$?; grep -v '^{' $OUT/ab_$s.txt | grep -v amdgpu.ids; if [ $rc -ne 0 ]; then exit $rc; fi
+done
+timeout -k 10 200 python tools/ab_variants.py --rounds 5 --scene refl --resolution 1080 --samples 4 $V/libyrt_nobun.so $V/libyrt_bun.so > $OUT/ab_c3.txt 2>&1
+rc=$?; grep -v '^{' $OUT/ab_c3.txt | grep -v amdgpu.ids; exit $rc

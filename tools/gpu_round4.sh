@@ -3,8 +3,9 @@
 #   bash tools/gpu_round4.sh A TAG   -m gpu suite, smoke, c4 counters + kernel stats, the
 #                                    default bench line (the three CPU legs), N=2 rehearsal
 #   bash tools/gpu_round4.sh B TAG   c3 and c5 counters + bench lines
-#   bash tools/gpu_round4.sh C TAG   counters of rank 0 of 2, 4 and 8 at c4 and at c5
-#                                    (bench.py --profile-rank): the N-rank lines' roofline
+#   bash tools/gpu_round4.sh C TAG   counters of rank 0 of 2, 4 and 8 at c4 (bench.py
+#                                    --profile-rank): the N-rank lines' roofline
+#   bash tools/gpu_round4.sh E TAG   the same at c5 (4096x4096, 16x16 spp)
 #   bash tools/gpu_round4.sh D TAG   instance1k / instance100k at c4 settings: counters
 #                                    + bench lines
 # Every GPU step has its own time limit; a failing step ends the script. The counter
@@ -47,6 +48,9 @@ elif [ "$PART" = C ]; then
   for n in 2 4 8; do
     pmc pmc_c4_r0of$n 150 --profile-rank 0/$n
     summ instance10000-1920x1080-s8-n$n-wavefront $OUT/pmc_c4_r0of$n
+  done
+elif [ "$PART" = E ]; then
+  for n in 2 4 8; do
     pmc pmc_c5_r0of$n 200 --profile-rank 0/$n --resolution 4096 --width 4096 --samples 16
     summ instance10000-4096x4096-s16-n$n-wavefront $OUT/pmc_c5_r0of$n
   done

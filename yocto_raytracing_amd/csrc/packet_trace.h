@@ -112,10 +112,14 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
 // (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
 template <int N>
 __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
-    static_assert(N == 3 || N == 4 || N == 5, "record count");
+    static_assert(N == 2 || N == 3 || N == 4 || N == 5, "record count");
     const f4* base = sgpr_ptr(base_);
     const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
-    if constexpr (N == 3) {
+    if constexpr (N == 2) {
+        sgpr8 a;
+        asm volatile("s_load_dwordx8 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1);
+    } else if constexpr (N == 3) {
         sgpr8 a;
         sgpr4 b;
         asm volatile("s_load_dwordx8 %0, %2, %3\n s_load_dwordx4 %1, %2, %3 offset:0x20\n s_waitcnt lgkmcnt(0)"
@@ -545,10 +549,31 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
 // trel (REL): the instance-level spine records relative to the origin that every lane's
 // ray shares (the camera's, for primary rays); the instance level is walked on them.
 // LDSN/lds (REL): the first LDSN records of trel staged in LDS by the caller (first_descend).
-template <bool COUNT, int BS = packet_block, bool REL = false, int LDSN = 0>
+//
+// List mode (REL, ln >= 0): instead of walking the instance tree, the walk takes the ln
+// leaves at lbase (wavefront.hip k_camera_lists: every instance-level leaf whose box a camera
+// ray of this pixel tile can pass, boxes relative to the camera origin, in the reference's
+// DFS order -- descending first slot, since the reference visits child start+1 before start
+// and the builder gives start the lower half) and tests each leaf's box with every live lane
+// at the lane's current tmax. That is the reference's computation: a leaf whose box passes
+// at the current tmax has every ancestor pass at the earlier (larger) tmax the reference
+// tested it with -- a box test is monotone in the box and in tmax -- so the reference reaches
+// it and tests it with this same tmax (the hits before it in DFS order being the same); a
+// leaf that fails, it either never reaches or tests and fails. Entries {lo - o, first}
+// {hi - o, count} (32 bytes).
+template <int OCT>
+__device__ __forceinline__ unsigned long long list_leaf_test(vec3f ci, float tmin, float tmax, const float4 (&e)[2],
+                                                             unsigned long long lanes) {
+    return ballot(box_oct<OCT>(vec3f{0.0f, 0.0f, 0.0f}, ci, tmin, tmax, e[0].x, e[0].y, e[0].z, e[1].x, e[1].y,
+                               e[1].z)) &
+           lanes;
+}
+// (LIST: the list mode is compiled in; without it the walk is the tree walk alone)
+template <bool COUNT, int BS = packet_block, bool REL = false, int LDSN = 0, bool LIST = false>
 __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3& wray, bool valid, hit_record& hr,
                                              work_counts& wc, const f4* trel = nullptr,
-                                             const float4* lds = nullptr) {
+                                             const float4* lds = nullptr, const f4* lbase = nullptr,
+                                             int ln = -1) {
     static_assert(spine_len == 2, "packet_first walks two-node spine records");
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
@@ -578,13 +603,57 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     vec3f icd, ici;
     enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
     const int ioct = wave_octant(ici, live);
+    const bool list = LIST && REL && !COUNT && ln >= 0;
+    // list mode: the list's address, length and next entry are parked in this wave's LDS
+    // slot between list steps, so they hold no registers through the instance walks
+    __shared__ int list_lds[BS / 64][4];
+    int* const lst = list_lds[threadIdx.x >> 6];
+    if (list) {
+        lst[0] = (int)(unsigned)(unsigned long long)lbase, lst[1] = (int)((unsigned long long)lbase >> 32);
+        lst[2] = ln, lst[3] = 0;
+    }
     for (;;) {
+        uint32_t lcl = 0;
+        if (list && level == 0) {
+            // ---- list mode: the next leaf some live lane passes, or the end ----
+            mask = 0;
+            asm volatile("" ::: "memory");
+            const f4* lb = (const f4*)((unsigned long long)(unsigned)uniform(lst[1]) << 32 | (unsigned)uniform(lst[0]));
+            const int lend = uniform(lst[2]);
+            int lnext = uniform(lst[3]);
+            while (lnext < lend) {
+                float4 e[2];
+                ld_records_at<2>(lb, (unsigned)(2 * lnext), e);
+                lnext++;
+                const unsigned long long lanes = live & ~done;
+                unsigned long long m;
+                switch (oct) {
+                    case 0: m = list_leaf_test<0>(ci, tmin, tmax, e, lanes); break;
+                    case 1: m = list_leaf_test<1>(ci, tmin, tmax, e, lanes); break;
+                    case 2: m = list_leaf_test<2>(ci, tmin, tmax, e, lanes); break;
+                    case 3: m = list_leaf_test<3>(ci, tmin, tmax, e, lanes); break;
+                    case 4: m = list_leaf_test<4>(ci, tmin, tmax, e, lanes); break;
+                    case 5: m = list_leaf_test<5>(ci, tmin, tmax, e, lanes); break;
+                    case 6: m = list_leaf_test<6>(ci, tmin, tmax, e, lanes); break;
+                    case 7: m = list_leaf_test<7>(ci, tmin, tmax, e, lanes); break;
+                    default: m = list_leaf_test<8>(ci, tmin, tmax, e, lanes); break;
+                }
+                if (m) {
+                    node = uniform(ibits(e[0].w));
+                    lcl = (uint32_t)uniform(ibits(e[1].w)) | leaf_bit;
+                    mask = m;
+                    break;
+                }
+            }
+            if (!mask) break;
+            lst[3] = lnext;
+            asm volatile("" ::: "memory");
+        } else {
         // ---- descent: one spine record per step, until a leaf or no passing lane ----
         DBG_CHECK(node >= 0 && (node % spine_record_bytes) == 0 && sp >= 0 && sp < 63 &&
                       (level == 0 ? node / spine_record_bytes < S.ntnodes
                                   : (int)((pbase - S.spair) / 4) + node / spine_record_bytes < S.nsnodes),
                   1, node, sp, level, (int)((pbase - S.spair) / 4), base);
-        uint32_t lcl = 0;
         const int floor = level ? base : 0;
 #define YRT_FD(o, R)                                                                                          \
     first_descend<o, COUNT, R, R ? LDSN : 0>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo,     \
@@ -615,6 +684,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
             }
         }
 #undef YRT_FD
+        }
         const unsigned long long lmask = mask;
         const int lstart = node, lcount = (int)(lcl & 0xffffu);
         // ---- the leaf reached, if any ----
@@ -709,6 +779,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 cd = wd;
                 ci = {wi_lds[0][threadIdx.x], wi_lds[1][threadIdx.x], wi_lds[2][threadIdx.x]};
                 oct = woct;
+                if (list) break;  // the next list entry (level 0 of list mode has no stack)
             }
             if (sp == 0) {
                 finished = true;
@@ -906,12 +977,14 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f 
 // child passes (mask = 0). LDSN > 0: the first LDSN records (the breadth-first top of
 // the instance tree, staged by the persistent kernel) are read from `lds` with
 // ds_read_b128 at a wave-uniform address; every other record through the scalar cache.
+// `base`: the records `cur` is a byte offset into (S.wnodes, or a shadow bundle's list,
+// packet_occluded_wide2)
 template <int OCT, int LDSN>
-__device__ __forceinline__ void wide_descend(const dev_scene_view& S, const float4* lds, vec3f co, vec3f ci,
+__device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, vec3f co, vec3f ci,
                                              float tmin, float tmax, uint32_t& cur, unsigned long long& mask,
                                              int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
                                              unsigned long long done, unsigned& nsteps) {
-    const f4* wbase = sgpr_ptr(S.wnodes);
+    const f4* wbase = sgpr_ptr(base);
     for (;;) {
         bool more;
 #ifdef YRT_WIDE_STATS
@@ -940,9 +1013,15 @@ __device__ __forceinline__ void wide_descend(const dev_scene_view& S, const floa
 // monotone in the box (NaN slabs included), so every leaf reached is one the reference
 // reaches, and the any-hit answer does not depend on the order. The instrumented
 // (COUNT) kernels use the binary walk instead, so work counts stay the reference's.
+//
+// tbase / troot: where the instance level's walk starts -- S.wnodes and the wide tree's root,
+// or the wide records of a shadow bundle's candidate leaves (wavefront.hip k_bundle_lists:
+// every instance-level leaf whose box a ray of the bundle can pass, so walking them instead
+// of the tree reaches the same leaves; the leaves' boxes and words are the tree's own)
 template <int LDSN = 0>
 __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid,
-                                                      const float4* lds = nullptr) {
+                                                      const float4* lds = nullptr, const f4* tbase = nullptr,
+                                                      uint32_t troot = 0) {
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
@@ -953,8 +1032,9 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     int stk_word = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
+    if (!tbase) tbase = S.wnodes, troot = (uint32_t)S.wtop_root;
     // the current item: a child word (a wide node's byte offset, or a leaf)
-    uint32_t cur = (uint32_t)S.wtop_root;
+    uint32_t cur = troot;
     unsigned long long mask = live;
     // the octant of the current level's rays when the whole wave shares it (8: mixed)
     const int woct = wave_octant(wi, live);
@@ -973,10 +1053,11 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
         // ---- descent through wide nodes until a leaf or no passing child ----
         if (!(cur & wide_leaf)) {
             const int wfloor = level ? base : 0;
-            DBG_CHECK(cur < (uint32_t)S.nwnodes * wide_record_bytes && sp >= 0 && sp < 61, 4, (int)cur, sp, level,
+            DBG_CHECK(((level == 0 && tbase != S.wnodes) || cur < (uint32_t)S.nwnodes * wide_record_bytes) && sp >= 0 &&
+                          sp < 61, 4, (int)cur, sp, level,
                       base, 0);
-#define YRT_WD(o) wide_descend<o, LDSN>(S, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, wfloor, done, \
-                                         level ? nsteps1 : nsteps0)
+#define YRT_WD(o) wide_descend<o, LDSN>(level ? S.wnodes : tbase, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, \
+                                         stk_mlo, stk_mhi, wfloor, done, level ? nsteps1 : nsteps0)
             switch (oct) {
                 case 0: YRT_WD(0); break;
                 case 1: YRT_WD(1); break;

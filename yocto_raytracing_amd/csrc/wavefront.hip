@@ -87,6 +87,15 @@ struct wf_buffers {
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
     int need_v;             // the scene has textures: the surface's v (surfv) is stored and read
+    // shadow bundles (level 0 of the persistent any-hit grid, k_bundle_lists)
+    int bundles;            // 1: this chunk's k_primary writes pbox and its shadow items walk lists
+    f4* pbox;               // per 64-sample item: {lo.xyz, -1 if a hit point is not finite} {hi.xyz, -}
+    int* lcount;            // per (bundle, light): candidate leaves, -1 = walk the tree
+    f4* lists;              // per (bundle, light): bundle_recs wide records (wide_record_bytes each)
+    // camera lists (the closest hit of the camera rays, k_camera_lists)
+    int cam_lists;          // 1: this chunk's camera rays walk their tile's list
+    int* ccount;            // per 8x8-pixel tile of the chunk: listed leaves, -1 = walk the tree
+    f4* clist;              // per tile: camera_list_max entries of 2 f4 {lo - o, first} {hi - o, count}
 };
 
 // Mirror levels are compacted into level_segments segments of B.seg slots: segment g of
@@ -322,13 +331,116 @@ __device__ __forceinline__ ray3 camera_ray_w(const dev_camera& cam, int W, int H
     return {o, d, ray_eps, flt_max};
 }
 
+// ---- shadow bundles ----
+// The shadow rays of one light from the samples of a bundle (bundle_g consecutive 64-sample
+// items: an 8x8-pixel tile at 8x8 spp) all run from points inside the box P of the bundle's
+// hit points towards one point, the light's position Lp (raytrace.cpp:129-133; the light
+// frame's rotation is the identity, so its ray is p -> transform_point(frame, pos0 - p) =
+// pos0 - p + o). Every such segment lies in the convex hull of P and Lp. k_bundle_lists
+// collects, per (bundle, light), the instance-level leaves of the any-hit tree whose box no
+// bounding plane of that hull separates by more than a margin far above the slab test's
+// rounding (its t values carry a few ulps of |t| <= |P - Lp|, the 1.00000024 fudge another
+// 2.4e-7): a leaf outside that list fails the exact box test of every ray of the bundle.
+// The walk then starts from the list (at most bundle_max leaves as a chain of wide records)
+// instead of the tree's root. It tests each listed leaf's own box,
+// exactly as the tree walk does, and reaches every leaf the tree walk reaches -- the
+// any-hit answer does not depend on which inner boxes were tested.
+// A bundle whose light is rotated, whose hit points are not finite or whose list would be
+// longer walks the tree.
+#ifndef YRT_SHADOW_BUNDLES
+#define YRT_SHADOW_BUNDLES 1
+#endif
+#ifndef YRT_BUNDLE_ITEMS
+#define YRT_BUNDLE_ITEMS 64  // 64-sample items per bundle (at most 64: one per lane of the list builder)
+#endif
+constexpr int bundle_g = YRT_BUNDLE_ITEMS;
+static_assert(bundle_g >= 1 && bundle_g <= 64, "one item per lane of k_bundle_lists");
+#ifndef YRT_BUNDLE_MIN_TOP
+#define YRT_BUNDLE_MIN_TOP 8  // bundles only when the instance level's wide tree has this many records
+#endif
+constexpr int bundle_max = 16;        // candidate leaves per list
+constexpr int bundle_recs = 5;        // wide records per list: a chain (3 + 3 + 3 + 3 + 4 leaves)
+constexpr int bundle_max_lights = 8;  // more lights: no bundles (the lists' memory grows with them)
+#ifndef YRT_CAMERA_LISTS
+#define YRT_CAMERA_LISTS 1  // camera rays walk per-tile leaf lists (k_camera_lists, packet_first's list mode)
+#endif
+#ifndef YRT_CAMERA_LIST_MAX
+#define YRT_CAMERA_LIST_MAX 32  // leaves per tile list (more: the tile's rays walk the tree)
+#endif
+constexpr int camera_list_max = YRT_CAMERA_LIST_MAX;
+
+// wave-wide min / max with DPP row rotations and row broadcasts (VALU only, no LDS round
+// trips): every row of 16 lanes folds itself, rows 1 and 3 take rows 0 and 2 (row_bcast:15),
+// rows 2 and 3 take row 1 (row_bcast:31); lane 63 then holds the result. The floats (no NaN
+// here) are folded as integers whose signed order is theirs (b ^ (b >> 31 & 0x7fffffff)), so
+// that each step is one v_min_i32 / v_max_i32 with the DPP source and no canonicalisation.
+// (the lanes of rows outside ROWS are left undefined: only row 3's lanes, which every step
+// writes, reach the result)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ int fkey(int b) { return b ^ ((b >> 31) & 0x7fffffff); }  // (its own inverse)
+template <bool MAX>
+__device__ __forceinline__ float wave_fold(float f) {
+    auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+    int v = fkey(__float_as_int(f));
+    v = op(v, dpp_i<0x121, 0xf>(v));  // row_ror:1
+    v = op(v, dpp_i<0x122, 0xf>(v));  // row_ror:2
+    v = op(v, dpp_i<0x124, 0xf>(v));  // row_ror:4
+    v = op(v, dpp_i<0x128, 0xf>(v));  // row_ror:8
+    v = op(v, dpp_i<0x142, 0xa>(v));  // row_bcast:15 into rows 1, 3
+    v = op(v, dpp_i<0x143, 0xc>(v));  // row_bcast:31 into rows 2, 3
+    return __int_as_float(fkey(__builtin_amdgcn_readlane(v, 63)));
+}
+__device__ __forceinline__ float wave_fmin(float v) { return wave_fold<false>(v); }
+__device__ __forceinline__ float wave_fmax(float v) { return wave_fold<true>(v); }
+// a box's six folds in lock step (their DPP steps interleave: no wait states between them)
+__device__ __forceinline__ void wave_box(float (&lo)[3], float (&hi)[3]) {
+    int v[6];
+    for (int a = 0; a < 3; a++) v[a] = fkey(__float_as_int(lo[a])), v[3 + a] = fkey(__float_as_int(hi[a]));
+#define YRT_BOX_STEP(CTRL, ROWS)                                                  \
+    {                                                                             \
+        int t[6];                                                                 \
+        for (int a = 0; a < 6; a++) t[a] = dpp_i<CTRL, ROWS>(v[a]);               \
+        for (int a = 0; a < 6; a++) v[a] = a < 3 ? min(v[a], t[a]) : max(v[a], t[a]); \
+    }
+    YRT_BOX_STEP(0x121, 0xf)
+    YRT_BOX_STEP(0x122, 0xf)
+    YRT_BOX_STEP(0x124, 0xf)
+    YRT_BOX_STEP(0x128, 0xf)
+    YRT_BOX_STEP(0x142, 0xa)
+    YRT_BOX_STEP(0x143, 0xc)
+#undef YRT_BOX_STEP
+    for (int a = 0; a < 3; a++) {
+        lo[a] = __int_as_float(fkey(__builtin_amdgcn_readlane(v[a], 63)));
+        hi[a] = __int_as_float(fkey(__builtin_amdgcn_readlane(v[3 + a], 63)));
+    }
+}
+
+// the box of this wave's hit points (the item idx / 64), for k_bundle_lists; called by
+// every lane of the wave
+__device__ __forceinline__ void store_item_box(const wf_buffers& B, int idx, bool has_p, vec3f p) {
+    const bool fin = has_p && __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
+    const bool bad = has_p && !fin;
+    float lo[3] = {fin ? p.x : INFINITY, fin ? p.y : INFINITY, fin ? p.z : INFINITY};
+    float hi[3] = {fin ? p.x : -INFINITY, fin ? p.y : -INFINITY, fin ? p.z : -INFINITY};
+    wave_box(lo, hi);
+    const bool any_bad = ballot(bad) != 0;
+    if ((threadIdx.x & 63) == 0) {
+        const int item = idx >> 6;
+        gstore(B.pbox, 2 * item, lo[0], lo[1], lo[2], any_bad ? -1.0f : 0.0f);
+        gstore(B.pbox, 2 * item + 1, hi[0], hi[1], hi[2], 0.0f);
+    }
+}
+
 #ifndef YRT_PRIMARY_REL
 #define YRT_PRIMARY_REL 1  // camera rays walk the instance level on camera-relative records
 #endif
 
 // ---- level 0: camera rays + closest hit + surface ----
 // the camera samples idx of one wave: eval_camera, closest hit, surface record
-template <bool COUNT, bool PACKET, typename SE, int BS = packet_block, int LDSN = 0>
+template <bool COUNT, bool PACKET, typename SE, int BS = packet_block, int LDSN = 0, bool LIST = false>
 __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const dev_render_args& A, const chunk_args& C,
                                                 const wf_buffers& B, tracer<false, COUNT, PACKET, SE, BS>& T, int idx,
                                                 work_counts& wc, const float4* lds = nullptr) {
@@ -349,22 +461,42 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     }
     hit_record hr = {-1, -1, {0, 0, 0, 0}, 0};
     // every camera ray starts at the camera origin (camera_ray): the packet walk tests the
-    // instance level on the records relative to it
+    // instance level on the records relative to it -- or, with camera lists, walks the list
+    // of the 8x8-pixel tile this wave's samples lie in (a wave straddling two tiles walks
+    // the tree)
     bool hit;
-    if constexpr (PACKET && YRT_PRIMARY_REL)
-        hit = packet_first<COUNT, BS, true, LDSN>(S, ray, valid, hr, wc, B.trel, lds);
-    else
+    if constexpr (PACKET && YRT_PRIMARY_REL) {
+        const f4* lbase = nullptr;
+        int ln = -1;
+        if (LIST && !COUNT) {
+            const int nsamp = C.npix * C.spp;
+            const int i0 = uniform(idx) & ~63, i1 = min(i0 + 63, nsamp - 1);
+            const int t0 = i0 / C.spp / (TILE * TILE), t1 = i1 / C.spp / (TILE * TILE);
+            // (a zero direction -- a camera with no extent -- walks the tree)
+            const bool zero_dir = valid && ray.d.x == 0.0f && ray.d.y == 0.0f && ray.d.z == 0.0f;
+            if (t0 == t1 && i0 < nsamp && !ballot(zero_dir)) {
+                ln = uniform(B.ccount[t0]);
+                lbase = B.clist + (size_t)t0 * camera_list_max * 2;
+            }
+        }
+        hit = packet_first<COUNT, BS, true, LDSN, LIST>(S, ray, valid, hr, wc, B.trel, lds, lbase, ln);
+    } else {
         hit = T.trace(S, ray, valid, hr, wc);
+    }
+    vec3f hp = {0, 0, 0};
     if (valid) {
         if (COUNT && hit) wc.hits++;
         if (YRT_HIT16) {
             store_hit16(B, idx, hit, hr);
+            if (YRT_SHADOW_BUNDLES && hit && B.bundles) hp = eval_surface(S, hr.slot, hr.ei, hr.ew).p;
         } else {
             surface sf = {};
             if (hit) sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
             store_surface(B, idx, hit, sf);
+            hp = sf.p;
         }
     }
+    if (YRT_SHADOW_BUNDLES && !COUNT && B.bundles) store_item_box(B, idx, valid && hit, hp);
     return valid;
 }
 
@@ -447,7 +579,8 @@ __device__ __forceinline__ unsigned xcd_item(unsigned q, unsigned xcd, unsigned 
     return q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
 }
 
-template <bool COUNT, bool PACKET, typename SE>
+// (LIST: the camera rays walk their tiles' lists, k_camera_lists)
+template <bool COUNT, bool PACKET, typename SE, bool LIST = false>
 __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A,
                                                                chunk_args C, wf_buffers B,
                                                                unsigned long long* counters) {
@@ -456,7 +589,7 @@ __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(
     auto T = make_tracer<false, COUNT, PACKET, SE>(lds);
     const int idx = (int)xcd_runs<YRT_XCD_CHUNK_PRIMARY>(blockIdx.x, gridDim.x) * BS + threadIdx.x;
     work_counts wc;
-    const bool valid = primary_samples<COUNT, PACKET, SE>(S, A, C, B, T, idx, wc);
+    const bool valid = primary_samples<COUNT, PACKET, SE, packet_block, 0, LIST>(S, A, C, B, T, idx, wc);
     flush_block<2, BS>(counters, {cnt_rays, cnt_samples}, {valid ? 1ull : 0ull, valid ? 1ull : 0ull});
     if (COUNT) flush_work(counters, wc);
 }
@@ -491,7 +624,7 @@ static_assert((YRT_PRIMARY_WAVES * 4 * 64) % YRT_PRIMARY_SP_BLOCK == 0, "whole b
 #ifndef YRT_PRIMARY_BLOCK_CHUNK
 #define YRT_PRIMARY_BLOCK_CHUNK 16  // (64: the same)
 #endif
-template <typename SE, int LDSN>
+template <typename SE, int LDSN, bool LIST = false>
 __global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_primary_persist(dev_scene_view S,
                                                                                 dev_render_args A, chunk_args C,
                                                                                 wf_buffers B,
@@ -525,7 +658,7 @@ __global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_pri
         if (it >= n_items) break;
         asm volatile("" ::: "memory");
         const bool valid =
-            primary_samples<false, true, SE, SPB, LDSN>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc, lds_rec);
+            primary_samples<false, true, SE, SPB, LDSN, LIST>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc, lds_rec);
         valid_n += (unsigned)__popcll(ballot(valid));
     }
     const unsigned long long mine = lane == 0 ? (unsigned long long)valid_n : 0ull;
@@ -637,6 +770,300 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     }
 }
 
+// one wave per (bundle, light): the candidate list (see above). Lane 16 s + k tests slot s of
+// the current wide record against sweep box k; the tree is walked with a lane-indexed stack.
+__global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffers B, int n_items) {
+    __shared__ float cand[4][bundle_max][8];  // per wave: lo.xyz, hi.xyz, word
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nl = S.nlights;
+    const int ngroups = (n_items + bundle_g - 1) / bundle_g;
+    const int gl = blockIdx.x * 4 + w;
+    if (gl >= ngroups * nl) return;  // (whole waves)
+    const int g = gl / nl, li = gl - g * nl;
+    // the bundle's box: lane l < bundle_g holds item g * bundle_g + l
+    float plx = INFINITY, ply = INFINITY, plz = INFINITY, phx = -INFINITY, phy = -INFINITY, phz = -INFINITY;
+    bool bad = false;
+    {
+        const int it = g * bundle_g + lane;
+        if (lane < bundle_g && it < n_items) {
+            const float4 a = ld4(B.pbox + 2 * it), b = ld4(B.pbox + 2 * it + 1);
+            plx = a.x, ply = a.y, plz = a.z, phx = b.x, phy = b.y, phz = b.z;
+            bad = a.w < 0.0f;
+        }
+    }
+    {
+        float lo[3] = {plx, ply, plz}, hi[3] = {phx, phy, phz};
+        wave_box(lo, hi);
+        plx = lo[0], ply = lo[1], plz = lo[2], phx = hi[0], phy = hi[1], phz = hi[2];
+    }
+    float4 lrec[5];
+    ld_records_at<5>(S.lights, (unsigned)(6 * li), lrec);
+    const bool ident = ubits(lrec[0].x) == 0x3f800000u && ubits(lrec[0].y) == 0 && ubits(lrec[0].z) == 0 &&
+                       ubits(lrec[1].x) == 0 && ubits(lrec[1].y) == 0x3f800000u && ubits(lrec[1].z) == 0 &&
+                       ubits(lrec[2].x) == 0 && ubits(lrec[2].y) == 0 && ubits(lrec[2].z) == 0x3f800000u;
+    const vec3f Lp = xyz(lrec[4]) + xyz(lrec[3]);
+    if (ballot(bad) || !ident || !(__builtin_isfinite(Lp.x) && __builtin_isfinite(Lp.y) && __builtin_isfinite(Lp.z))) {
+        if (lane == 0) B.lcount[gl] = -1;
+        return;
+    }
+    if (!(plx <= phx)) {  // no hit point in the bundle: no shadow ray
+        if (lane == 0) B.lcount[gl] = 0;
+        return;
+    }
+    const float M = fmaxf(fmaxf(fmaxf(fabsf(plx), fabsf(ply)), fmaxf(fabsf(plz), fabsf(phx))),
+                          fmaxf(fmaxf(fabsf(phy), fabsf(phz)), fmaxf(fmaxf(fabsf(Lp.x), fabsf(Lp.y)), fabsf(Lp.z))));
+    const float eps = 1e-3f + 3e-5f * M;
+    // The rays' hull: the convex hull of P and Lp. Lane j = lane % 16 of each slot's group
+    // holds one of its bounding planes: j == 0 the hull's box (P's box with Lp), j = 1..12 the
+    // plane through Lp and box edge j - 1 of P when that edge is on P's silhouette seen from
+    // Lp (one adjacent face turned towards Lp, the other away). A child box is dropped only
+    // when some lane finds it entirely outside its plane by more than the margin -- a
+    // conservative test (the hull's other separating axes are not tried).
+    const int j = lane & 15;
+    const float P0[3] = {plx, ply, plz}, P1[3] = {phx, phy, phz}, L3[3] = {Lp.x, Lp.y, Lp.z};
+    const float bxl = fminf(plx, Lp.x) - eps, bxh = fmaxf(phx, Lp.x) + eps;
+    const float byl = fminf(ply, Lp.y) - eps, byh = fmaxf(phy, Lp.y) + eps;
+    const float bzl = fminf(plz, Lp.z) - eps, bzh = fmaxf(phz, Lp.z) + eps;
+    float nx = 0.0f, ny = 0.0f, nz = 0.0f, nd = 0.0f, nmargin = INFINITY;
+    if (j >= 1 && j <= 12) {
+        const int e = j - 1, a = e >> 2, b = (a + 1) % 3, c = (a + 2) % 3;
+        const bool bh = e & 1, ch = (e >> 1) & 1;  // the edge's sides on axes b and c
+        // a face faces Lp when Lp lies strictly outside the box on that face's side
+        const bool fb = bh ? L3[b] > P1[b] : L3[b] < P0[b];
+        const bool fc = ch ? L3[c] > P1[c] : L3[c] < P0[c];
+        if (fb != fc) {
+            float e0[3], e1[3];
+            e0[a] = P0[a], e1[a] = P1[a];
+            e0[b] = e1[b] = bh ? P1[b] : P0[b];
+            e0[c] = e1[c] = ch ? P1[c] : P0[c];
+            const float ux = e1[0] - e0[0], uy = e1[1] - e0[1], uz = e1[2] - e0[2];
+            const float vx = L3[0] - e0[0], vy = L3[1] - e0[1], vz = L3[2] - e0[2];
+            nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
+            // the box centre on the inner (negative) side
+            const float cx = 0.5f * (P0[0] + P1[0]) - e0[0], cy = 0.5f * (P0[1] + P1[1]) - e0[1],
+                        cz = 0.5f * (P0[2] + P1[2]) - e0[2];
+            if (nx * cx + ny * cy + nz * cz > 0.0f) nx = -nx, ny = -ny, nz = -nz;
+            nd = nx * e0[0] + ny * e0[1] + nz * e0[2];
+            nmargin = (fabsf(nx) + fabsf(ny) + fabsf(nz)) * (eps + 1e-5f * M);
+        }
+    }
+    const int s = lane >> 4;  // the slot this lane tests
+    const f4* wbase = sgpr_ptr(S.wnodes);
+    int stk = 0, sp = 0, nc = 0;
+    bool overflow = false;
+    uint32_t cur = (uint32_t)S.wtop_root;
+    for (;;) {
+        float4 r[7];
+        ld_wide_record(wbase, cur, r);
+        const float4 rs[7] = {r[0], r[1], r[2], r[3], r[4], r[5], r[6]};
+        auto comp = [&](float4 v) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; };
+        const float clx = comp(rs[0]), cly = comp(rs[1]), clz = comp(rs[2]);
+        const float chx = comp(rs[3]), chy = comp(rs[4]), chz = comp(rs[5]);
+        // separated: entirely outside this lane's plane (a NaN bound never separates: the
+        // reference's select-based slab test can pass a box with a NaN plane)
+        bool sep;
+        if (j == 0) {
+            sep = clx > bxh || chx < bxl || cly > byh || chy < byl || clz > bzh || chz < bzl;
+        } else {
+            const float mn = nx * (nx > 0.0f ? clx : chx) + ny * (ny > 0.0f ? cly : chy) + nz * (nz > 0.0f ? clz : chz);
+            sep = mn - nd > nmargin;
+        }
+        const unsigned long long sm = ballot(sep);
+        unsigned long long m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t wq = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
+            if (wq != wide_leaf && !((sm >> (16 * q)) & 0xffffull)) m |= 0xffffull << (16 * q);
+        }
+
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (!((m >> (16 * q)) & 0xffffull)) continue;
+            const uint32_t word = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
+            if (word & wide_leaf) {
+                if (nc == bundle_max) {
+                    overflow = true;
+                    continue;
+                }
+                if (lane == 0) {
+                    const float4 c = {q == 0 ? r[0].x : q == 1 ? r[0].y : q == 2 ? r[0].z : r[0].w,
+                                      q == 0 ? r[1].x : q == 1 ? r[1].y : q == 2 ? r[1].z : r[1].w,
+                                      q == 0 ? r[2].x : q == 1 ? r[2].y : q == 2 ? r[2].z : r[2].w, 0};
+                    const float4 d = {q == 0 ? r[3].x : q == 1 ? r[3].y : q == 2 ? r[3].z : r[3].w,
+                                      q == 0 ? r[4].x : q == 1 ? r[4].y : q == 2 ? r[4].z : r[4].w,
+                                      q == 0 ? r[5].x : q == 1 ? r[5].y : q == 2 ? r[5].z : r[5].w, 0};
+                    float* e = cand[w][nc];
+                    e[0] = c.x, e[1] = c.y, e[2] = c.z, e[3] = d.x, e[4] = d.y, e[5] = d.z, e[6] = __uint_as_float(word);
+                }
+                nc++;
+            } else {
+                stk = writelane(stk, (int)word, sp);
+                sp++;
+            }
+        }
+        if (overflow || sp == 0) break;
+        sp--;
+        cur = (uint32_t)__builtin_amdgcn_readlane(stk, sp);
+    }
+    if (overflow) {
+        if (lane == 0) B.lcount[gl] = -1;
+        return;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's candidate stores, before any lane reads them
+    // the list as wide records at B.lists + gl * bundle_recs: up to 4 leaves in the root;
+    // more in up to 4 child records of 4, the root's slot c holding child c's box (the union
+    // of its leaves' boxes) and its byte offset from B.lists
+    // a chain: record r holds leaves 3r, 3r + 1, 3r + 2 and, in slot 3, record r + 1 (its box
+    // the union of every leaf after them) -- the last record holds the last <= 4 leaves
+    const int nrec = nc <= 4 ? 1 : 1 + (nc - 4 + 2) / 3;
+    const uint32_t rec0 = (uint32_t)gl * bundle_recs;
+    // lane q (< nrec * 4) builds slot q % 4 of record q / 4 -- then lanes write the rows
+    __shared__ float slot[4][bundle_recs * 4][8];
+    if (lane < nrec * 4) {
+        const int rq = lane / 4, c = lane % 4;
+        float v[7] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY, __uint_as_float(wide_leaf)};
+        if (rq == nrec - 1 || c < 3) {  // a leaf
+            const int e = 3 * rq + c;
+            if (e < nc)
+                for (int q = 0; q < 7; q++) v[q] = cand[w][e][q];
+        } else {  // the rest of the chain
+            for (int e = 3 * rq + 3; e < nc; e++)
+                for (int q = 0; q < 3; q++) v[q] = fminf(v[q], cand[w][e][q]), v[q + 3] = fmaxf(v[q + 3], cand[w][e][q + 3]);
+            v[6] = __uint_as_float((rec0 + rq + 1) * (uint32_t)wide_record_bytes);
+        }
+        for (int q = 0; q < 7; q++) slot[w][lane][q] = v[q];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < nrec * 8) {
+        const int rq = lane / 8, row = lane % 8;
+        const float* a = slot[w][4 * rq];
+        float4 o = row < 7 ? make_float4(a[row], a[8 + row], a[16 + row], a[24 + row]) : make_float4(0, 0, 0, 0);
+        reinterpret_cast<float4*>(B.lists)[(size_t)(rec0 + rq) * 8 + row] = o;
+    }
+    if (lane == 0) B.lcount[gl] = nc;
+}
+
+// ---- camera lists: per 8x8-pixel tile of the chunk, the instance-level leaves whose box a
+// camera ray of the tile can pass (packet_first's list mode). The tile's rays start at the
+// camera origin O and run through its pixels' rectangle [i0, i1 + 1] x [j0, j1 + 1] of the
+// image plane (the samples lie strictly inside it, raytrace.cpp:236-239), so they lie in the
+// cone from O through the rectangle's four corners. One wave per tile walks the any-hit
+// tree (its leaves are the reference's, its inner boxes unions of them): lane 16 s + k tests
+// slot s against cone plane k (k < 4), and a box is dropped when it lies outside a plane
+// by more than a margin above the slab test's rounding. The leaves go out in the reference's
+// DFS order (descending first slot), boxes relative to O (the same fp32 (bound - o) as the
+// REL records).
+__global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_render_args A, chunk_args C, wf_buffers B) {
+    __shared__ float cand[4][camera_list_max][8];  // per wave: lo.xyz, first, hi.xyz, count
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ntiles = C.npix / (TILE * TILE);
+    const int t = blockIdx.x * 4 + w;
+    if (t >= ntiles) return;  // (whole waves)
+    const long long T = C.pix0 / (TILE * TILE) + t;
+    const int lx0 = (int)(T % C.tiles_x) * TILE, ly0 = (int)(T / C.tiles_x) * TILE;
+    // the tile's image columns and rows (bands interleave the rows: take their range)
+    const int i0 = A.x0 + lx0, i1 = A.x0 + lx0 + TILE - 1;
+    int jr;
+    {
+        const int ly = ly0 + (lane < TILE ? lane : 0);
+        const int b = ly / A.band, r = ly % A.band;
+        jr = A.y0 + (b * A.band_stride + A.band_offset) * A.band + r;
+    }
+    int j0 = jr, j1 = jr;
+    for (int off = 1; off < 64; off <<= 1) j0 = min(j0, __shfl_xor(j0, off, 64)), j1 = max(j1, __shfl_xor(j1, off, 64));
+    j0 = uniform(j0), j1 = uniform(j1);
+    const float u0 = (float)i0 / (float)A.width, u1 = (float)(i1 + 1) / (float)A.width;
+    const float v0 = (float)j0 / (float)A.height, v1 = (float)(j1 + 1) / (float)A.height;
+    const dev_camera& K = A.cam;
+    auto dir = [&](float u, float v) {
+        return vec3f{(u - 0.5f) * K.w * K.xx + (v - 0.5f) * K.h * K.yx - K.focus * K.zx,
+                     (u - 0.5f) * K.w * K.xy + (v - 0.5f) * K.h * K.yy - K.focus * K.zy,
+                     (u - 0.5f) * K.w * K.xz + (v - 0.5f) * K.h * K.yz - K.focus * K.zz};
+    };
+    const vec3f O = {K.ox, K.oy, K.oz};
+    // the cone plane of this lane (k = lane % 16 < 4): through O and corners k, k + 1
+    const int k = lane & 15;
+    const float cu[4] = {u0, u1, u1, u0}, cv[4] = {v0, v0, v1, v1};
+    vec3f n = {0, 0, 0};
+    if (k < 4) {
+        const vec3f a = dir(cu[k], cv[k]), b = dir(cu[(k + 1) & 3], cv[(k + 1) & 3]);
+        n = cross(a, b);
+        const vec3f c = dir(0.5f * (u0 + u1), 0.5f * (v0 + v1));
+        if (dot(n, c) > 0.0f) n = n * -1.0f;  // the cone on the negative side
+    }
+    const f4* wbase = sgpr_ptr(S.wnodes);
+    // the scene's extent (the root record's children) for the margin
+    float M = fmaxf(fmaxf(fabsf(O.x), fabsf(O.y)), fabsf(O.z));
+    {
+        float4 r[7];
+        ld_wide_record(wbase, (uint32_t)S.wtop_root, r);
+        for (int q = 0; q < 6; q++)
+            M = fmaxf(M, fmaxf(fmaxf(fabsf(r[q].x), fabsf(r[q].y)), fmaxf(fabsf(r[q].z), fabsf(r[q].w))));
+    }
+    const float eps = 1e-3f + 3e-5f * M;
+    const float margin = (fabsf(n.x) + fabsf(n.y) + fabsf(n.z)) * eps;
+    const int s = lane >> 4;
+    int stk = 0, sp = 0, nc = 0;
+    bool overflow = false;
+    uint32_t cur = (uint32_t)S.wtop_root;
+    for (;;) {
+        float4 r[7];
+        ld_wide_record(wbase, cur, r);
+        auto comp = [&](float4 v) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; };
+        const float clx = comp(r[0]) - O.x, cly = comp(r[1]) - O.y, clz = comp(r[2]) - O.z;
+        const float chx = comp(r[3]) - O.x, chy = comp(r[4]) - O.y, chz = comp(r[5]) - O.z;
+        // outside this lane's plane (a NaN bound never separates)
+        const float mn = n.x * (n.x > 0.0f ? clx : chx) + n.y * (n.y > 0.0f ? cly : chy) + n.z * (n.z > 0.0f ? clz : chz);
+        const bool sep = k < 4 && mn > margin;
+        const unsigned long long sm = ballot(sep);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t word = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
+            if (word == wide_leaf || ((sm >> (16 * q)) & 0xffffull)) continue;
+            if (word & wide_leaf) {
+                if (nc == camera_list_max) {
+                    overflow = true;
+                    continue;
+                }
+                if (lane == 0) {
+                    float* e = cand[w][nc];
+                    e[0] = q == 0 ? r[0].x : q == 1 ? r[0].y : q == 2 ? r[0].z : r[0].w;
+                    e[1] = q == 0 ? r[1].x : q == 1 ? r[1].y : q == 2 ? r[1].z : r[1].w;
+                    e[2] = q == 0 ? r[2].x : q == 1 ? r[2].y : q == 2 ? r[2].z : r[2].w;
+                    e[3] = __int_as_float((int)(word & wide_index_mask));
+                    e[4] = q == 0 ? r[3].x : q == 1 ? r[3].y : q == 2 ? r[3].z : r[3].w;
+                    e[5] = q == 0 ? r[4].x : q == 1 ? r[4].y : q == 2 ? r[4].z : r[4].w;
+                    e[6] = q == 0 ? r[5].x : q == 1 ? r[5].y : q == 2 ? r[5].z : r[5].w;
+                    e[7] = __int_as_float((int)((word >> wide_count_shift) & 7u));
+                }
+                nc++;
+            } else {
+                stk = writelane(stk, (int)word, sp);
+                sp++;
+            }
+        }
+        if (overflow || sp == 0) break;
+        sp--;
+        cur = (uint32_t)__builtin_amdgcn_readlane(stk, sp);
+    }
+    if (overflow) {
+        if (lane == 0) B.ccount[t] = -1;
+        return;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's candidate stores, before any lane reads them
+    if (lane < nc) {
+        // rank in the reference's DFS order: descending first slot (the slots are distinct)
+        const int first = __float_as_int(cand[w][lane][3]);
+        int rank = 0;
+        for (int q = 0; q < nc; q++) rank += __float_as_int(cand[w][q][3]) > first ? 1 : 0;
+        const float* e = cand[w][lane];
+        f4* out = B.clist + ((size_t)t * camera_list_max + rank) * 2;
+        out[0] = {e[0] - O.x, e[1] - O.y, e[2] - O.z, e[3]};
+        out[1] = {e[4] - O.x, e[5] - O.y, e[6] - O.z, e[7]};
+    }
+    if (lane == 0) B.ccount[t] = nc;
+}
+
 // ---- shadow rays, persistent: a grid of SP_BLOCK-thread blocks that fills the chip once;
 // every wave walks its own share of the (64-sample block, light) items, so no block
 // launch, block retirement or per-block counter flush happens per item (level 0 with
@@ -711,7 +1138,20 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
             }
         }
         rays += (unsigned)__popcll(ballot(valid));
-        const bool occ = packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes);
+        bool occ;
+        int lc = -1;  // the bundle's list: its leaf count, -1 = walk the tree
+        if (YRT_SHADOW_BUNDLES && LDSN == 0 && B.bundles) {
+            const int gl = (bx / bundle_g) * nl + li;
+            lc = __builtin_amdgcn_readfirstlane(B.lcount[gl]);
+        }
+        const f4* tbase = S.wnodes;
+        uint32_t troot = (uint32_t)S.wtop_root;
+        if (lc > 0) {  // (the host turns bundles off with LDS-staged records: LDSN == 0 here)
+            tbase = B.lists;
+            troot = (uint32_t)(((bx / bundle_g) * nl + li) * bundle_recs * wide_record_bytes);
+        }
+        // lc == 0: no leaf can be passed by these rays, none is occluded
+        occ = lc == 0 ? false : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
     }
     const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
@@ -1011,16 +1451,32 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // the per-level, per-segment mirror-ray counters (seg_counter)
 size_t count_bytes(int nlevels) { return sizeof(int) * ((size_t)nlevels + 1) * level_segments * count_stride; }
 
-size_t workspace_bytes(int cap, int nlights, int nlevels) {
+// shadow bundles: items (64-sample blocks) and bundles of a chunk of cap samples
+size_t bundle_items(int cap) { return ((size_t)cap + 63) / 64; }
+size_t bundle_count(int cap) { return (bundle_items(cap) + bundle_g - 1) / bundle_g; }
+int bundle_lights(int nlights) { return nlights <= bundle_max_lights ? nlights : 0; }
+
+// camera lists: 8x8-pixel tiles of a chunk of cap samples at spp samples per pixel
+size_t camera_tiles(int cap, int spp) { return ((size_t)cap / (size_t)spp + TILE * TILE - 1) / (TILE * TILE); }
+
+size_t workspace_bytes(int cap, int spp, int nlights, int nlevels) {
     size_t c = (size_t)cap;
     size_t b = align_up(count_bytes(nlevels)) + align_up(16 * sizeof(unsigned));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
+    if (YRT_SHADOW_BUNDLES) {
+        const size_t gl = bundle_count(cap) * bundle_lights(nlights);
+        b += align_up(32 * bundle_items(cap)) + align_up(4 * gl) + align_up((size_t)bundle_recs * wide_record_bytes * gl);
+    }
+    if (YRT_CAMERA_LISTS) {
+        const size_t nt = camera_tiles(cap, spp);
+        b += align_up(4 * nt) + align_up(nt * camera_list_max * 32);
+    }
     // levels >= 1: ray_o, ray_d; levels < last: rec0, rec1 (one slab each)
     if (nlevels > 1) b += 4 * align_up((size_t)(nlevels - 1) * 16 * c);
     return b;
 }
 
-wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
+wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
     wf_buffers B = {};
     char* p = (char*)base;
     size_t c = (size_t)cap;
@@ -1036,6 +1492,17 @@ wf_buffers carve(void* base, int cap, int nlights, int nlevels) {
     B.surfv = (float*)take(4 * c);
     B.occl = (unsigned char*)take(c * std::max(nlights, 1));
     B.rad = (f4*)take(16 * c);
+    if (YRT_SHADOW_BUNDLES) {
+        const size_t gl = bundle_count(cap) * bundle_lights(nlights);
+        B.pbox = (f4*)take(32 * bundle_items(cap));
+        B.lcount = (int*)take(4 * gl);
+        B.lists = (f4*)take((size_t)bundle_recs * wide_record_bytes * gl);
+    }
+    if (YRT_CAMERA_LISTS) {
+        const size_t nt = camera_tiles(cap, spp);
+        B.ccount = (int*)take(4 * nt);
+        B.clist = (f4*)take(nt * camera_list_max * 32);
+    }
     if (nlevels > 1) {
         const size_t slab = (size_t)(nlevels - 1) * 16 * c;
         B.ray_o_ = (f4*)take(slab);
@@ -1076,7 +1543,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     // segments) at most cap / 8 + 8 * 256
     auto seg_of = [&](int pix) { return pix * spp / level_segments + level_segments * WF_BLOCK; };
     auto cap_of = [&](int pix) { return nlevels > 1 ? level_segments * seg_of(pix) : pix * spp; };
-    auto bytes_of = [&](long long tgt) { return workspace_bytes(cap_of(cap_for(tgt)), ds.nlights, nlevels); };
+    auto bytes_of = [&](long long tgt) { return workspace_bytes(cap_of(cap_for(tgt)), spp, ds.nlights, nlevels); };
     // the free-memory query (a driver round trip) only when the workspace must grow: a
     // steady frame loop reuses the workspace it already has
     if (bytes_of(target) > ds.work_bytes) {
@@ -1092,7 +1559,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     const int pix_per_chunk = cap_for(target);
     const int seg = seg_of(pix_per_chunk);
     const int cap = cap_of(pix_per_chunk);
-    const size_t need = workspace_bytes(cap, ds.nlights, nlevels);
+    const size_t need = workspace_bytes(cap, spp, ds.nlights, nlevels);
     if (need > ds.work_bytes) {
         if (ds.work) (void)hipFree(ds.work);
         ds.work = nullptr;
@@ -1101,7 +1568,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         if (e != hipSuccess) return e;
         ds.work_bytes = need;
     }
-    wf_buffers B = carve(ds.work, cap, ds.nlights, nlevels);
+    wf_buffers B = carve(ds.work, cap, spp, ds.nlights, nlevels);
     B.trel = ds.trel;
     B.seg = seg;
     B.need_v = ds.view.ntextures > 0;
@@ -1127,6 +1594,17 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             hipError_t e = hipMemsetAsync(B.count, 0, count_bytes(nlevels), stream);
             if (e != hipSuccess) return e;
         }
+        constexpr int TB = shadow_block<PACKET>();
+        const int tgrid = (nsamp + TB - 1) / TB;
+        // level 0's shadow rays run on the persistent any-hit grid (k_shadow_persist)
+        const bool shadow_persist = !COUNT && PACKET && ds.wide_ok && TB == 64 && ds.nlights > 0 &&
+                                    (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS;
+        // ... and walk the bundles' candidate lists (k_bundle_lists) instead of the tree
+        B.bundles = YRT_SHADOW_BUNDLES && YRT_SHADOW_LDS_RECORDS == 0 && shadow_persist &&
+                    bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
+        // the camera rays walk their tiles' leaf lists (k_camera_lists)
+        B.cam_lists = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
+                      ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
         int t = T.begin(phase_primary, stream);
         if (PACKET && pix0 == 0) {
             // the camera-relative instance-level records of this render (timed with the
@@ -1135,8 +1613,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
                                ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);
         }
-        constexpr int TB = shadow_block<PACKET>();
-        const int tgrid = (nsamp + TB - 1) / TB;
+        if (B.cam_lists) {
+            const int nt = C.npix / (TILE * TILE);
+            hipLaunchKernelGGL(k_camera_lists, dim3((nt + 3) / 4), dim3(256), 0, stream, ds.view, A, C, B);
+        }
         bool persist = false;
         if constexpr (!COUNT && PACKET) {
             persist = ((long long)nsamp + 63) / 64 >= (long long)YRT_PRIMARY_PERSIST_MIN_ITEMS;
@@ -1144,13 +1624,23 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 hipError_t e = hipMemsetAsync(B.queue + 8, 0, 8 * sizeof(unsigned), stream);
                 if (e != hipSuccess) return e;
                 const int nb = ds.num_cus * (YRT_PRIMARY_WAVES * 4 * 64 / YRT_PRIMARY_SP_BLOCK);
-                hipLaunchKernelGGL((k_primary_persist<SE, YRT_PRIMARY_LDS_RECORDS>), dim3(nb),
-                                   dim3(YRT_PRIMARY_SP_BLOCK), 0, stream, ds.view, A, C, B, counters);
+                if (B.cam_lists)
+                    hipLaunchKernelGGL((k_primary_persist<SE, YRT_PRIMARY_LDS_RECORDS, true>), dim3(nb),
+                                       dim3(YRT_PRIMARY_SP_BLOCK), 0, stream, ds.view, A, C, B, counters);
+                else
+                    hipLaunchKernelGGL((k_primary_persist<SE, YRT_PRIMARY_LDS_RECORDS, false>), dim3(nb),
+                                       dim3(YRT_PRIMARY_SP_BLOCK), 0, stream, ds.view, A, C, B, counters);
             }
         }
-        if (!persist)
-            hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE>), dim3((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK),
-                               dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view, A, C, B, counters);
+        if (!persist) {
+            const dim3 pg((nsamp + YRT_PRIMARY_BLOCK - 1) / YRT_PRIMARY_BLOCK);
+            if (B.cam_lists)
+                hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE, true>), pg, dim3(YRT_PRIMARY_BLOCK), 0, stream, ds.view,
+                                   A, C, B, counters);
+            else
+                hipLaunchKernelGGL((k_primary<COUNT, PACKET, SE, false>), pg, dim3(YRT_PRIMARY_BLOCK), 0, stream,
+                                   ds.view, A, C, B, counters);
+        }
         T.end(t, stream);
         // levels run: a level with no mirror rays ends the chunk's recursion. The host
         // reads each level's ray count (written by the previous level's k_shade) without
@@ -1174,8 +1664,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 t = T.begin(phase_shadow, stream);
                 // level 0 only: at c3 the mirror levels' compacted samples trace faster with the
                 // hardware's dealing (shadow 1.64 -> 1.72 ms with them persistent)
-                if (!COUNT && PACKET && ds.wide_ok && TB == 64 && level == 0 &&
-                    (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS) {
+                if (level == 0 && shadow_persist) {
+                    if (B.bundles) {
+                        const long long nw = (long long)bundle_count(nsamp) * ds.nlights;
+                        hipLaunchKernelGGL(k_bundle_lists, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream, ds.view,
+                                           B, tgrid);
+                    }
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
                     {
