@@ -772,6 +772,8 @@ void device_scene_destroy(device_scene* ds) {
     if (ds->work) (void)hipFree(ds->work);
     if (ds->level_count_ev) (void)hipEventDestroy(ds->level_count_ev);
     if (ds->level_count_host) (void)hipHostFree(ds->level_count_host);
+    if (ds->list_stats_ev) (void)hipEventDestroy(ds->list_stats_ev);
+    if (ds->list_stats_host) (void)hipHostFree(ds->list_stats_host);
     delete ds;
 }
 

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "packet_trace.h"
@@ -96,6 +98,7 @@ struct wf_buffers {
     int cam_lists;          // 1: this chunk's camera rays walk their tile's list
     int* ccount;            // per 8x8-pixel tile of the chunk: listed leaves, -1 = walk the tree
     f4* clist;              // per tile: camera_list_max entries of 2 f4 {lo - o, first} {hi - o, count}
+    unsigned long long* lstats;  // the render's list sums (k_list_stats)
 };
 
 // Mirror levels are compacted into level_segments segments of B.seg slots: segment g of
@@ -368,6 +371,13 @@ constexpr int bundle_max_lights = 8;  // more lights: no bundles (the lists' mem
 #define YRT_CAMERA_LIST_MAX 32  // leaves per tile list (more: the tile's rays walk the tree)
 #endif
 constexpr int camera_list_max = YRT_CAMERA_LIST_MAX;
+#ifndef YRT_LIST_MAX_MEAN
+// a kind of list stays on while its lists average at most this many leaves (a list that fell
+// back to the tree counts as its capacity + 1): longer lists cost more than the tree walk they
+// replace (A/B: instance10000 3.8 / 4.3 leaves per camera / bundle list, -6 % per frame;
+// instance100k 17.8 / 9.2, +2 to +4 %)
+#define YRT_LIST_MAX_MEAN 6
+#endif
 
 // wave-wide min / max with DPP row rotations and row broadcasts (VALU only, no LDS round
 // trips): every row of 16 lanes folds itself, rows 1 and 3 take rows 0 and 2 (row_bcast:15),
@@ -1064,6 +1074,34 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     if (lane == 0) B.ccount[t] = nc;
 }
 
+// the sums of one chunk's list lengths into B.lstats (a list that fell back to the tree counts
+// as camera_list_max + 1 / bundle_max + 1 entries), added to the render's totals: a grid-stride
+// sum per block, four atomics per block
+__global__ __launch_bounds__(256) void k_list_stats(wf_buffers B, int ntiles, int nlists) {
+    __shared__ unsigned long long part[4][256 / 64];
+    unsigned long long v[4] = {0, 0, 0, 0};
+    const int stride = gridDim.x * 256;
+    if (B.cam_lists)
+        for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < ntiles; i += stride) {
+            const int n = B.ccount[i];
+            v[0] += n < 0 ? camera_list_max + 1 : n, v[1]++;
+        }
+    if (B.bundles)
+        for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < nlists; i += stride) {
+            const int n = B.lcount[i];
+            v[2] += n < 0 ? bundle_max + 1 : n, v[3]++;
+        }
+    for (int q = 0; q < 4; q++) {
+        const unsigned long long t = wave_sum(v[q]);
+        if ((threadIdx.x & 63) == 0) part[q][threadIdx.x >> 6] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const unsigned long long t = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
+        if (t) atomicAdd(B.lstats + threadIdx.x, t);
+    }
+}
+
 // ---- shadow rays, persistent: a grid of SP_BLOCK-thread blocks that fills the chip once;
 // every wave walks its own share of the (64-sample block, light) items, so no block
 // launch, block retirement or per-block counter flush happens per item (level 0 with
@@ -1461,7 +1499,7 @@ size_t camera_tiles(int cap, int spp) { return ((size_t)cap / (size_t)spp + TILE
 
 size_t workspace_bytes(int cap, int spp, int nlights, int nlevels) {
     size_t c = (size_t)cap;
-    size_t b = align_up(count_bytes(nlevels)) + align_up(16 * sizeof(unsigned));
+    size_t b = align_up(count_bytes(nlevels)) + align_up(16 * sizeof(unsigned)) + align_up(4 * sizeof(unsigned long long));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
     if (YRT_SHADOW_BUNDLES) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
@@ -1487,6 +1525,7 @@ wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
     };
     B.count = (int*)take(count_bytes(nlevels));
     B.queue = (unsigned*)take(16 * sizeof(unsigned));
+    B.lstats = (unsigned long long*)take(4 * sizeof(unsigned long long));
     B.surf0 = (f4*)take(16 * c);
     B.surf1 = (f4*)take(16 * c);
     B.surfv = (float*)take(4 * c);
@@ -1572,6 +1611,19 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     B.trel = ds.trel;
     B.seg = seg;
     B.need_v = ds.view.ntextures > 0;
+    // the list sums of an earlier render, if they have arrived: keep or drop each kind of list
+    // (every 32 renders both are tried again)
+    if (ds.list_stats_ev && hipEventQuery(ds.list_stats_ev) == hipSuccess) {
+        const unsigned long long* st = ds.list_stats_host;
+        static const bool debug = getenv("YRT_LIST_DEBUG") != nullptr;  // diagnostic: the lists' mean lengths
+        if (debug)
+            fprintf(stderr, "yrt lists: camera %llu entries / %llu tiles, bundles %llu entries / %llu lists\n", st[0],
+                    st[1], st[2], st[3]);
+        if (st[1]) ds.camera_lists_on = st[0] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[1];
+        if (st[3]) ds.bundles_on = st[2] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[3];
+    }
+    if (++ds.list_renders >= 32) ds.camera_lists_on = ds.bundles_on = true, ds.list_renders = 0;
+    bool list_stats = false;
     if (nlevels > 1 && !ds.level_count_host) {
         hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int) * level_segments * count_stride,
                                      hipHostMallocDefault);
@@ -1601,10 +1653,15 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                     (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS;
         // ... and walk the bundles' candidate lists (k_bundle_lists) instead of the tree
         B.bundles = YRT_SHADOW_BUNDLES && YRT_SHADOW_LDS_RECORDS == 0 && shadow_persist &&
-                    bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
+                    bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP && ds.bundles_on;
         // the camera rays walk their tiles' leaf lists (k_camera_lists)
         B.cam_lists = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
-                      ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
+                      ds.view.nwtop >= YRT_BUNDLE_MIN_TOP && ds.camera_lists_on;
+        if ((B.cam_lists || B.bundles) && !list_stats) {
+            list_stats = true;
+            hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);
+            if (e != hipSuccess) return e;
+        }
         int t = T.begin(phase_primary, stream);
         if (PACKET && pix0 == 0) {
             // the camera-relative instance-level records of this render (timed with the
@@ -1724,6 +1781,23 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                C, B, out);
             T.end(t, stream);
         }
+        if (B.cam_lists || B.bundles)
+            hipLaunchKernelGGL(k_list_stats, dim3(64), dim3(256), 0, stream, B, C.npix / (TILE * TILE),
+                               (int)(bundle_count(nsamp) * (size_t)ds.nlights));
+    }
+    if (list_stats) {
+        if (!ds.list_stats_host) {
+            hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+            if (e != hipSuccess) return e;
+        }
+        if (!ds.list_stats_ev) {
+            hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipMemcpyAsync(ds.list_stats_host, B.lstats, 4 * sizeof(unsigned long long),
+                                      hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipEventRecord(ds.list_stats_ev, stream);
+        if (e != hipSuccess) return e;
     }
     return hipGetLastError();
 }

@@ -66,6 +66,14 @@ struct device_scene {
     // mirror levels: the next level's ray count, copied back behind the level's kernels
     int* level_count_host = nullptr;  // pinned
     hipEvent_t level_count_ev = nullptr;
+    // the candidate lists (wavefront.hip k_camera_lists / k_bundle_lists) pay only when they
+    // are short: each render sums its lists' lengths on the device and copies the sums back
+    // behind its kernels; the next render reads them (if they have arrived) and keeps or
+    // drops each kind of list. Both ways give the same image.
+    unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
+    hipEvent_t list_stats_ev = nullptr;
+    bool camera_lists_on = true, bundles_on = true;
+    int list_renders = 0;  // renders since the lists were last re-tried
     phase_timer timer;
 };
 
