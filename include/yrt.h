@@ -99,6 +99,7 @@ enum {
     YRT_PHASE_FOLD = 4,       /* reflection fold */
     YRT_PHASE_ACCUMULATE = 5, /* ordered per-pixel sum */
     YRT_PHASE_MEGAKERNEL = 6, /* the one-kernel path */
+    YRT_PHASE_LISTS = 7,      /* per-render camera-relative records and candidate-leaf lists */
     YRT_PHASE_COUNT = 8
 };
 typedef struct yrt_timings {

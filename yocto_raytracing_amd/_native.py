@@ -70,7 +70,7 @@ class Stats(C.Structure):
         "wave_prim_visits", "shadow_wave_node_visits")]
 
 
-PHASES = ("primary", "shadow", "shade", "bounce", "fold", "accumulate", "megakernel", "unused")
+PHASES = ("primary", "shadow", "shade", "bounce", "fold", "accumulate", "megakernel", "lists")
 
 
 class Timings(C.Structure):

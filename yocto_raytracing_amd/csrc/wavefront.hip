@@ -1662,7 +1662,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);
             if (e != hipSuccess) return e;
         }
-        int t = T.begin(phase_primary, stream);
+        int t = T.begin(phase_lists, stream);
         if (PACKET && pix0 == 0) {
             // the camera-relative instance-level records of this render (timed with the
             // primary phase, whose walk reads them)
@@ -1674,6 +1674,8 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             const int nt = C.npix / (TILE * TILE);
             hipLaunchKernelGGL(k_camera_lists, dim3((nt + 3) / 4), dim3(256), 0, stream, ds.view, A, C, B);
         }
+        T.end(t, stream);
+        t = T.begin(phase_primary, stream);
         bool persist = false;
         if constexpr (!COUNT && PACKET) {
             persist = ((long long)nsamp + 63) / 64 >= (long long)YRT_PRIMARY_PERSIST_MIN_ITEMS;
@@ -1718,15 +1720,17 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             }
             if (ds.nlights > 0) {
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
+                if (level == 0 && shadow_persist && B.bundles) {  // the bundles' candidate lists
+                    t = T.begin(phase_lists, stream);
+                    const long long nw = (long long)bundle_count(nsamp) * ds.nlights;
+                    hipLaunchKernelGGL(k_bundle_lists, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream, ds.view, B,
+                                       tgrid);
+                    T.end(t, stream);
+                }
                 t = T.begin(phase_shadow, stream);
                 // level 0 only: at c3 the mirror levels' compacted samples trace faster with the
                 // hardware's dealing (shadow 1.64 -> 1.72 ms with them persistent)
                 if (level == 0 && shadow_persist) {
-                    if (B.bundles) {
-                        const long long nw = (long long)bundle_count(nsamp) * ds.nlights;
-                        hipLaunchKernelGGL(k_bundle_lists, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream, ds.view,
-                                           B, tgrid);
-                    }
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
                     {
@@ -1781,9 +1785,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                C, B, out);
             T.end(t, stream);
         }
-        if (B.cam_lists || B.bundles)
+        if (B.cam_lists || B.bundles) {
+            t = T.begin(phase_lists, stream);
             hipLaunchKernelGGL(k_list_stats, dim3(64), dim3(256), 0, stream, B, C.npix / (TILE * TILE),
                                (int)(bundle_count(nsamp) * (size_t)ds.nlights));
+            T.end(t, stream);
+        }
     }
     if (list_stats) {
         if (!ds.list_stats_host) {

@@ -22,6 +22,7 @@ enum render_phase {
     phase_fold = 4,      // reflection fold (k_fold_children)
     phase_accumulate = 5,
     phase_megakernel = 6,
+    phase_lists = 7,     // per-render records and candidate lists (k_relative_records, k_camera_lists, k_bundle_lists, k_list_stats)
     phase_count = 8
 };
 
