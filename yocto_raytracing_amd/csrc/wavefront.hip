@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 #include "packet_trace.h"
@@ -1611,9 +1612,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     B.trel = ds.trel;
     B.seg = seg;
     B.need_v = ds.view.ntextures > 0;
-    // the list sums of an earlier render, if they have arrived: keep or drop each kind of list
-    // (every 32 renders both are tried again)
-    if (ds.list_stats_ev && hipEventQuery(ds.list_stats_ev) == hipSuccess) {
+    // a new view is probed (below); otherwise the list sums of an earlier render, if they have
+    // arrived, keep or drop each kind of list
+    if (ds.lists_probed && (memcmp(&ds.probe_cam, &A.cam, sizeof(dev_camera)) != 0 || ds.probe_w != A.width ||
+                            ds.probe_h != A.height || ds.probe_spp != spp))
+        ds.lists_probed = false;
+    if (ds.lists_probed && ds.list_stats_ev && hipEventQuery(ds.list_stats_ev) == hipSuccess) {
         const unsigned long long* st = ds.list_stats_host;
         static const bool debug = getenv("YRT_LIST_DEBUG") != nullptr;  // diagnostic: the lists' mean lengths
         if (debug)
@@ -1622,8 +1626,15 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         if (st[1]) ds.camera_lists_on = st[0] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[1];
         if (st[3]) ds.bundles_on = st[2] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[3];
     }
-    if (++ds.list_renders >= 32) ds.camera_lists_on = ds.bundles_on = true, ds.list_renders = 0;
     bool list_stats = false;
+    if (!ds.list_stats_host) {
+        hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+    }
+    if (!ds.list_stats_ev) {
+        hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
     if (nlevels > 1 && !ds.level_count_host) {
         hipError_t e = hipHostMalloc((void**)&ds.level_count_host, sizeof(int) * level_segments * count_stride,
                                      hipHostMallocDefault);
@@ -1652,11 +1663,33 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         const bool shadow_persist = !COUNT && PACKET && ds.wide_ok && TB == 64 && ds.nlights > 0 &&
                                     (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS;
         // ... and walk the bundles' candidate lists (k_bundle_lists) instead of the tree
-        B.bundles = YRT_SHADOW_BUNDLES && YRT_SHADOW_LDS_RECORDS == 0 && shadow_persist &&
-                    bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP && ds.bundles_on;
+        const bool bundles_possible = YRT_SHADOW_BUNDLES && YRT_SHADOW_LDS_RECORDS == 0 && shadow_persist &&
+                                      bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
         // the camera rays walk their tiles' leaf lists (k_camera_lists)
-        B.cam_lists = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
-                      ds.view.nwtop >= YRT_BUNDLE_MIN_TOP && ds.camera_lists_on;
+        const bool cam_lists_possible = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
+                                        ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
+        if (cam_lists_possible && !ds.lists_probed && pix0 == 0) {
+            // probe this view: sum the first chunk's camera lists and wait for the sum; both kinds
+            // of list follow it (their lengths go together: instance10000 3.8 / 4.3 leaves,
+            // instance100k 17.8 / 9.2), later renders refine each from its own sums
+            wf_buffers Bp = B;
+            Bp.cam_lists = 1, Bp.bundles = 0;
+            hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);
+            if (e != hipSuccess) return e;
+            const int nt = C.npix / (TILE * TILE);
+            hipLaunchKernelGGL(k_camera_lists, dim3((nt + 3) / 4), dim3(256), 0, stream, ds.view, A, C, Bp);
+            hipLaunchKernelGGL(k_list_stats, dim3(64), dim3(256), 0, stream, Bp, nt, 0);
+            e = hipMemcpyAsync(ds.list_stats_host, B.lstats, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) return e;
+            const unsigned long long* st = ds.list_stats_host;
+            const bool on = st[1] == 0 || st[0] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[1];
+            ds.camera_lists_on = ds.bundles_on = on;
+            ds.lists_probed = true, ds.probe_cam = A.cam, ds.probe_w = A.width, ds.probe_h = A.height, ds.probe_spp = spp;
+        }
+        B.cam_lists = cam_lists_possible && ds.camera_lists_on;
+        B.bundles = bundles_possible && ds.bundles_on;
         if ((B.cam_lists || B.bundles) && !list_stats) {
             list_stats = true;
             hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);
@@ -1793,14 +1826,6 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         }
     }
     if (list_stats) {
-        if (!ds.list_stats_host) {
-            hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
-            if (e != hipSuccess) return e;
-        }
-        if (!ds.list_stats_ev) {
-            hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
-            if (e != hipSuccess) return e;
-        }
         hipError_t e = hipMemcpyAsync(ds.list_stats_host, B.lstats, 4 * sizeof(unsigned long long),
                                       hipMemcpyDeviceToHost, stream);
         if (e == hipSuccess) e = hipEventRecord(ds.list_stats_ev, stream);

@@ -74,7 +74,11 @@ struct device_scene {
     unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
     hipEvent_t list_stats_ev = nullptr;
     bool camera_lists_on = true, bundles_on = true;
-    int list_renders = 0;  // renders since the lists were last re-tried
+    // the view the lists were last probed for (a first render, or a new camera or image size,
+    // probes: its first chunk's camera lists are summed before its walks run)
+    bool lists_probed = false;
+    dev_camera probe_cam = {};
+    int probe_w = 0, probe_h = 0, probe_spp = 0;
     phase_timer timer;
 };
 
