@@ -92,7 +92,7 @@ struct wf_buffers {
     int need_v;             // the scene has textures: the surface's v (surfv) is stored and read
     // shadow bundles (level 0 of the persistent any-hit grid, k_bundle_lists)
     int bundles;            // 1: this chunk's k_primary writes pbox and its shadow items walk lists
-    f4* pbox;               // per 64-sample item, per 16-lane row: {lo.xyz, -1 if a hit point is not finite} {hi.xyz, -}
+    f4* pbox;               // per 64-sample item: {lo.xyz, -1 if a hit point is not finite} {hi.xyz, -}
     int* lcount;            // per (bundle, light): candidate leaves, -1 = walk the tree
     f4* lists;              // per (bundle, light): bundle_recs wide records (wide_record_bytes each)
     // camera lists (the closest hit of the camera rays, k_camera_lists)
@@ -407,8 +407,6 @@ __device__ __forceinline__ float wave_fold(float f) {
 __device__ __forceinline__ float wave_fmin(float v) { return wave_fold<false>(v); }
 __device__ __forceinline__ float wave_fmax(float v) { return wave_fold<true>(v); }
 // a box's six folds in lock step (their DPP steps interleave: no wait states between them)
-// (ROWS: stop after the row folds; every lane then holds its 16-lane row's box)
-template <bool ROWS = false>
 __device__ __forceinline__ void wave_box(float (&lo)[3], float (&hi)[3]) {
     int v[6];
     for (int a = 0; a < 3; a++) v[a] = fkey(__float_as_int(lo[a])), v[3 + a] = fkey(__float_as_int(hi[a]));
@@ -422,10 +420,6 @@ __device__ __forceinline__ void wave_box(float (&lo)[3], float (&hi)[3]) {
     YRT_BOX_STEP(0x122, 0xf)
     YRT_BOX_STEP(0x124, 0xf)
     YRT_BOX_STEP(0x128, 0xf)
-    if (ROWS) {
-        for (int a = 0; a < 3; a++) lo[a] = __int_as_float(fkey(v[a])), hi[a] = __int_as_float(fkey(v[3 + a]));
-        return;
-    }
     YRT_BOX_STEP(0x142, 0xa)
     YRT_BOX_STEP(0x143, 0xc)
 #undef YRT_BOX_STEP
@@ -435,20 +429,19 @@ __device__ __forceinline__ void wave_box(float (&lo)[3], float (&hi)[3]) {
     }
 }
 
-// the boxes of this wave's hit points (the item idx / 64), one per 16-lane row (the row folds
-// only: k_bundle_lists unions the four), for k_bundle_lists; called by every lane of the wave
+// the box of this wave's hit points (the item idx / 64), for k_bundle_lists; called by
+// every lane of the wave
 __device__ __forceinline__ void store_item_box(const wf_buffers& B, int idx, bool has_p, vec3f p) {
     const bool fin = has_p && __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
     const bool bad = has_p && !fin;
     float lo[3] = {fin ? p.x : INFINITY, fin ? p.y : INFINITY, fin ? p.z : INFINITY};
     float hi[3] = {fin ? p.x : -INFINITY, fin ? p.y : -INFINITY, fin ? p.z : -INFINITY};
-    wave_box<true>(lo, hi);
+    wave_box(lo, hi);
     const bool any_bad = ballot(bad) != 0;
-    const int lane = threadIdx.x & 63;
-    if ((lane & 15) == 0) {
-        const int row = 2 * (4 * (idx >> 6) + (lane >> 4));
-        gstore(B.pbox, row, lo[0], lo[1], lo[2], any_bad ? -1.0f : 0.0f);
-        gstore(B.pbox, row + 1, hi[0], hi[1], hi[2], 0.0f);
+    if ((threadIdx.x & 63) == 0) {
+        const int item = idx >> 6;
+        gstore(B.pbox, 2 * item, lo[0], lo[1], lo[2], any_bad ? -1.0f : 0.0f);
+        gstore(B.pbox, 2 * item + 1, hi[0], hi[1], hi[2], 0.0f);
     }
 }
 
@@ -804,12 +797,9 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
     {
         const int it = g * bundle_g + lane;
         if (lane < bundle_g && it < n_items) {
-            for (int r = 0; r < 4; r++) {  // the item's four row boxes
-                const float4 a = ld4(B.pbox + 2 * (4 * it + r)), b = ld4(B.pbox + 2 * (4 * it + r) + 1);
-                plx = fminf(plx, a.x), ply = fminf(ply, a.y), plz = fminf(plz, a.z);
-                phx = fmaxf(phx, b.x), phy = fmaxf(phy, b.y), phz = fmaxf(phz, b.z);
-                bad = bad || a.w < 0.0f;
-            }
+            const float4 a = ld4(B.pbox + 2 * it), b = ld4(B.pbox + 2 * it + 1);
+            plx = a.x, ply = a.y, plz = a.z, phx = b.x, phy = b.y, phz = b.z;
+            bad = a.w < 0.0f;
         }
     }
     {
@@ -1514,7 +1504,7 @@ size_t workspace_bytes(int cap, int spp, int nlights, int nlevels) {
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
     if (YRT_SHADOW_BUNDLES) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
-        b += align_up(128 * bundle_items(cap)) + align_up(4 * gl) + align_up((size_t)bundle_recs * wide_record_bytes * gl);
+        b += align_up(32 * bundle_items(cap)) + align_up(4 * gl) + align_up((size_t)bundle_recs * wide_record_bytes * gl);
     }
     if (YRT_CAMERA_LISTS) {
         const size_t nt = camera_tiles(cap, spp);
@@ -1544,7 +1534,7 @@ wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
     B.rad = (f4*)take(16 * c);
     if (YRT_SHADOW_BUNDLES) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
-        B.pbox = (f4*)take(128 * bundle_items(cap));
+        B.pbox = (f4*)take(32 * bundle_items(cap));
         B.lcount = (int*)take(4 * gl);
         B.lists = (f4*)take((size_t)bundle_recs * wide_record_bytes * gl);
     }
