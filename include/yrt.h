@@ -69,6 +69,7 @@ typedef struct yrt_render_params {
  *   MEGAKERNEL      one kernel, one lane per pixel walking the reference's loops
  *   WAVEFRONT_LANE  kernel per stage, one independent BVH walk per lane */
 enum { YRT_ALGO_WAVEFRONT = 0, YRT_ALGO_MEGAKERNEL = 1, YRT_ALGO_WAVEFRONT_LANE = 2 };
+enum { YRT_LISTS_AUTO = 0, YRT_LISTS_ON = 1, YRT_LISTS_OFF = 2 };
 
 /* counters accumulated by the last yrt_render / yrt_trace_* on a scene handle */
 typedef struct yrt_stats {
@@ -193,6 +194,17 @@ int yrt_trace_any(yrt_scene* ds, const float* rays, int n, unsigned char* hit, i
  * (default) = the render path's wave-coherent closest-hit walk and 4-wide any-hit walk;
  * YRT_ALGO_MEGAKERNEL / YRT_ALGO_WAVEFRONT_LANE = one independent walk per lane */
 int yrt_scene_set_trace_algorithm(yrt_scene* ds, int algorithm);
+/* per-tile candidate lists of yrt_render (camera lists and shadow
+ * bundles; identical images either way): YRT_LISTS_AUTO (default) probes each new view and
+ * keeps the lists while they average <= 6 leaves, YRT_LISTS_ON builds them whenever the
+ * scene allows (an instance tree of >= 8 wide records, unrotated point lights), YRT_LISTS_OFF
+ * never builds them */
+int yrt_scene_set_tile_lists(yrt_scene* ds, int mode);
+/* the lists' state after the last yrt_render on this handle (synchronises with it):
+ * whether each kind is in use, and sums[4] = {camera-list entries, camera lists, bundle-list
+ * entries, bundle lists} of the last render that built lists (a list that fell back to the
+ * tree counts as its capacity + 1) */
+int yrt_scene_tile_lists(yrt_scene* ds, int* camera_on, int* bundles_on, unsigned long long* sums);
 /* counters of the last render/trace call on this handle (synchronises the stream) */
 int yrt_last_stats(yrt_scene* ds, yrt_stats* stats);
 /* per-phase GPU times of the last yrt_render with p->timing = 1 (synchronises) */

@@ -28,6 +28,7 @@ __all__ = [
 ]
 
 ALGORITHMS = {"wavefront": 0, "megakernel": 1, "wavefront_lane": 2}
+TILE_LISTS = {"auto": 0, "on": 1, "off": 2}
 INFO_FIELDS = ("cameras", "textures", "materials", "shapes", "instances", "lights",
                "bvh_nodes", "bvh_depth", "shape_bvh_depth", "triangles", "lines", "points")
 
@@ -179,6 +180,18 @@ class DeviceScene:
     def set_trace_algorithm(self, algorithm: str) -> None:
         """walks used by intersect_first/intersect_any on this scene (identical results)"""
         check(N.lib.yrt_scene_set_trace_algorithm(self._h, ALGORITHMS[algorithm]), "set_trace_algorithm")
+
+    def set_tile_lists(self, mode: str) -> None:
+        """per-tile candidate lists of render_into: "auto" (default: probed per view), "on", "off"
+        -- identical images either way"""
+        check(N.lib.yrt_scene_set_tile_lists(self._h, TILE_LISTS[mode]), "set_tile_lists")
+
+    def tile_lists(self) -> dict:
+        """the lists the last render used, and the sums of the last render that built any"""
+        cam, bun, sums = C.c_int(), C.c_int(), (C.c_ulonglong * 4)()
+        check(N.lib.yrt_scene_tile_lists(self._h, C.byref(cam), C.byref(bun), sums), "tile_lists")
+        return {"camera": bool(cam.value), "bundles": bool(bun.value), "camera_entries": int(sums[0]),
+                "camera_lists": int(sums[1]), "bundle_entries": int(sums[2]), "bundle_lists": int(sums[3])}
 
     @property
     def device_bytes(self) -> int:

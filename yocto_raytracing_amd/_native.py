@@ -118,6 +118,8 @@ _sig = {
     "yrt_trace_first": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp]),
     "yrt_trace_any": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int, _vp]),
     "yrt_scene_set_trace_algorithm": (C.c_int, [_vp, C.c_int]),
+    "yrt_scene_set_tile_lists": (C.c_int, [_vp, C.c_int]),
+    "yrt_scene_tile_lists": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_ulonglong)]),
     "yrt_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "yrt_last_timings": (C.c_int, [_vp, C.POINTER(Timings)]),
     "yrt_tonemap": (C.c_int, [_vp, C.c_int, _vp, C.c_int, _vp]),

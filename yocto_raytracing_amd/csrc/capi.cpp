@@ -401,6 +401,26 @@ int yrt_scene_set_trace_algorithm(yrt_scene* s, int algorithm) {
     return YRT_OK;
 }
 
+int yrt_scene_set_tile_lists(yrt_scene* s, int mode) {
+    if (!s || mode < YRT_LISTS_AUTO || mode > YRT_LISTS_OFF) return YRT_ERR_INVALID_ARG;
+    s->ds->lists_mode = mode;
+    return YRT_OK;
+}
+
+int yrt_scene_tile_lists(yrt_scene* s, int* camera_on, int* bundles_on, unsigned long long* sums) {
+    if (!s) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::device_scene& ds = *s->ds;
+        hip_check(hipSetDevice(ds.device), "hipSetDevice");
+        if (ds.list_stats_ev) hip_check(hipEventSynchronize(ds.list_stats_ev), "list sums");
+        if (camera_on) *camera_on = ds.last_camera_lists;
+        if (bundles_on) *bundles_on = ds.last_bundles;
+        if (sums)
+            for (int i = 0; i < 4; i++) sums[i] = ds.list_stats_host ? ds.list_stats_host[i] : 0;
+        return YRT_OK;
+    });
+}
+
 size_t yrt_scene_device_bytes(const yrt_scene* s) { return s && s->ds ? s->ds->arena_bytes : 0; }
 
 void yrt_scene_free(yrt_scene* s) {

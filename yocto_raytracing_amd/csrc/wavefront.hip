@@ -1627,6 +1627,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         if (st[3]) ds.bundles_on = st[2] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[3];
     }
     bool list_stats = false;
+    ds.last_camera_lists = ds.last_bundles = false;
     if (!ds.list_stats_host) {
         hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
         if (e != hipSuccess) return e;
@@ -1659,16 +1660,18 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         }
         constexpr int TB = shadow_block<PACKET>();
         const int tgrid = (nsamp + TB - 1) / TB;
-        // level 0's shadow rays run on the persistent any-hit grid (k_shadow_persist)
+        // level 0's shadow rays run on the persistent any-hit grid (k_shadow_persist) -- on
+        // any frame size when the caller forces the lists on (the bundles live there)
         const bool shadow_persist = !COUNT && PACKET && ds.wide_ok && TB == 64 && ds.nlights > 0 &&
-                                    (long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS;
+                                    ((long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS ||
+                                     ds.lists_mode == 1);
         // ... and walk the bundles' candidate lists (k_bundle_lists) instead of the tree
         const bool bundles_possible = YRT_SHADOW_BUNDLES && YRT_SHADOW_LDS_RECORDS == 0 && shadow_persist &&
                                       bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
         // the camera rays walk their tiles' leaf lists (k_camera_lists)
         const bool cam_lists_possible = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
                                         ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
-        if (cam_lists_possible && !ds.lists_probed && pix0 == 0) {
+        if (cam_lists_possible && ds.lists_mode == 0 && !ds.lists_probed && pix0 == 0) {
             // probe this view: sum the first chunk's camera lists and wait for the sum; both kinds
             // of list follow it (their lengths go together: instance10000 3.8 / 4.3 leaves,
             // instance100k 17.8 / 9.2), later renders refine each from its own sums
@@ -1688,8 +1691,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             ds.camera_lists_on = ds.bundles_on = on;
             ds.lists_probed = true, ds.probe_cam = A.cam, ds.probe_w = A.width, ds.probe_h = A.height, ds.probe_spp = spp;
         }
-        B.cam_lists = cam_lists_possible && ds.camera_lists_on;
-        B.bundles = bundles_possible && ds.bundles_on;
+        // (YRT_LISTS_ON / _OFF: the caller's choice, yrt_scene_set_tile_lists)
+        B.cam_lists = cam_lists_possible && (ds.lists_mode == 1 || (ds.lists_mode == 0 && ds.camera_lists_on));
+        B.bundles = bundles_possible && (ds.lists_mode == 1 || (ds.lists_mode == 0 && ds.bundles_on));
+        ds.last_camera_lists |= B.cam_lists != 0, ds.last_bundles |= B.bundles != 0;
         if ((B.cam_lists || B.bundles) && !list_stats) {
             list_stats = true;
             hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);

@@ -74,6 +74,8 @@ struct device_scene {
     unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
     hipEvent_t list_stats_ev = nullptr;
     bool camera_lists_on = true, bundles_on = true;
+    int lists_mode = 0;  // YRT_LISTS_AUTO (the above) / YRT_LISTS_ON / YRT_LISTS_OFF (yrt_scene_set_tile_lists)
+    bool last_camera_lists = false, last_bundles = false;  // what the last render used
     // the view the lists were last probed for (a first render, or a new camera or image size,
     // probes: its first chunk's camera lists are summed before its walks run)
     bool lists_probed = false;
