@@ -3,6 +3,7 @@ rule 24: cross-process timings are not comparable).
 
     python tools/build_variants.py NAME:DEFINES ...      # build the .so files
     python tools/ab_variants.py --rounds 5 lib_a.so lib_b.so ...
+    python tools/ab_variants.py lib.so@on lib.so@off        # the same library, tile lists forced
 
 Each library is loaded with RTLD_LOCAL (own kernels, shared HIP runtime), renders
 the c4 frame (instance10000, 1080p, 8x8 spp) into a device buffer on its own
@@ -49,6 +50,7 @@ def main():
     ap.add_argument("--scene", default="instance10000")
     ap.add_argument("--resolution", type=int, default=1080)
     ap.add_argument("--samples", type=int, default=8)
+    ap.add_argument("--width", type=int, default=0, help="image width (0: the camera's aspect)")
     ap.add_argument("--algorithm", type=int, default=0)
     ap.add_argument("--count", action="store_true", help="also print the work counters of one pass")
     ap.add_argument("--share", default="0/1", help="R/N: render rank R's 8-row bands of an N-rank split")
@@ -59,15 +61,20 @@ def main():
     out = None
     runs = []
     scene = str(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.yrtscene").encode()
-    for path in a.libs:
+    for spec in a.libs:
+        path, _, lists = spec.partition("@")  # lib.so@auto|on|off: yrt_scene_set_tile_lists
         lib, N = bind(path)
         hs, ds = C.c_void_p(), C.c_void_p()
         assert lib.yrt_scene_load(scene, C.byref(hs)) == 0, lib.yrt_last_error()
         assert lib.yrt_host_scene_build_bvh(hs, 0) == 0
         assert lib.yrt_scene_upload(hs, 0, C.byref(ds)) == 0, lib.yrt_last_error()
+        if lists:
+            lib.yrt_scene_set_tile_lists.argtypes = [C.c_void_p, C.c_int]
+            assert lib.yrt_scene_set_tile_lists(ds, {"auto": 0, "on": 1, "off": 2}[lists]) == 0
         p = N.RenderParams()
         lib.yrt_render_params_default(C.byref(p))
         p.resolution, p.samples, p.algorithm, p.timing = a.resolution, a.samples, a.algorithm, 1
+        p.width = a.width
         w, h = C.c_int(), C.c_int()
         lib.yrt_image_size(ds, C.byref(p), C.byref(w), C.byref(h))
         rank, world = (int(v) for v in a.share.split("/"))
@@ -79,7 +86,7 @@ def main():
             h = C.c_int(p.tile_h)
         if out is None:
             out = torch.empty((h.value, w.value, 4), dtype=torch.float32, device="cuda")
-        runs.append((Path(path).name, lib, N, ds, p, torch.cuda.Stream()))
+        runs.append((Path(path).name + (f"@{lists}" if lists else ""), lib, N, ds, p, torch.cuda.Stream()))
     res = {name: {} for name, *_ in runs}
     digest = {}
     for r in range(a.rounds + 1):  # round 0 = warmup

@@ -627,10 +627,13 @@ static_assert((YRT_PRIMARY_WAVES * 4 * 64) % YRT_PRIMARY_SP_BLOCK == 0, "whole b
 #endif
 #ifndef YRT_PRIMARY_PERSIST_MIN_ITEMS
 // A/B against k_primary (items = 64-sample blocks; profiles/r3/ab_primary_persist): 2.07 M
-// (c4) primary 11.55 -> 11.37 ms; instance100k 27.16 -> 27.01; 0.52 M (c3; rank 0 of 4)
-// and 0.26 M (rank 0 of 8) unchanged. (Holding the arguments in registers instead: 62 SGPR
-// and 12 VGPR spills, c4 unchanged.)
-#define YRT_PRIMARY_PERSIST_MIN_ITEMS 1000000
+// (c4) primary 11.55 -> 11.37 ms; instance100k 27.16 -> 27.01. Round 4
+// (profiles/r4/ab_persist): the band shares of an N-rank split, which the old 1 M threshold
+// sent to k_primary, lose most: c4 rank 0 of 8 / 4 primary 2.89 -> 1.52 / 4.60 -> 2.89 ms,
+// instance100k rank 0 of 8 13.91 -> 3.74; c3 1.14 -> 1.10, 640x360 c4 1.49 -> 0.98; c1/c2
+// equal. The timed path is persistent at every size. (Holding the arguments in registers
+// instead: 62 SGPR and 12 VGPR spills, c4 unchanged.)
+#define YRT_PRIMARY_PERSIST_MIN_ITEMS 0
 #endif
 #ifndef YRT_PRIMARY_BLOCK_CHUNK
 #define YRT_PRIMARY_BLOCK_CHUNK 16  // (64: the same)
