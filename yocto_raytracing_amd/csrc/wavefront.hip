@@ -590,6 +590,19 @@ __device__ __forceinline__ unsigned xcd_item(unsigned q, unsigned xcd, unsigned 
     return q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
 }
 
+#ifdef YRT_TAIL_STATS
+// diagnostic build only (tools/tail_stats.py): per wave of the persistent grids, its start
+// and end on the 100 MHz constant clock, the items it took and its XCD (vector stores)
+static __device__ unsigned long long g_tail[2][8192][4];
+__device__ __forceinline__ void tail_record(int k, unsigned long long t0, unsigned items) {
+    const unsigned gw = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
+    if ((threadIdx.x & 63) == 0 && gw < 8192u) {
+        unsigned long long* e = g_tail[k][gw];
+        e[0] = t0, e[1] = __builtin_amdgcn_s_memrealtime(), e[2] = items, e[3] = blockIdx.x % 8u;
+    }
+}
+#endif
+
 // (LIST: the camera rays walk their tiles' lists, k_camera_lists)
 template <bool COUNT, bool PACKET, typename SE, bool LIST = false>
 __global__ __launch_bounds__(YRT_PRIMARY_BLOCK, YRT_TRACE_WAVES) void k_primary(dev_scene_view S, dev_render_args A,
@@ -666,15 +679,25 @@ __global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_pri
     const unsigned n_items = (unsigned)((C.npix * C.spp + 63) / 64);
     work_counts wc;
     unsigned valid_n = 0;  // wave-uniform: camera samples of this wave
+#ifdef YRT_TAIL_STATS
+    const unsigned long long tail_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned tail_items = 0;
+#endif
     for (;;) {
         const unsigned q = chunk_ring_next<CS>(ring, counter, lane);
         const unsigned it = xcd_item<YRT_XCD_CHUNK_PRIMARY>(q, xcd, n_items);
         if (it >= n_items) break;
+#ifdef YRT_TAIL_STATS
+        tail_items++;
+#endif
         asm volatile("" ::: "memory");
         const bool valid =
             primary_samples<false, true, SE, SPB, LDSN, LIST>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc, lds_rec);
         valid_n += (unsigned)__popcll(ballot(valid));
     }
+#ifdef YRT_TAIL_STATS
+    tail_record(0, tail_t0, tail_items);
+#endif
     const unsigned long long mine = lane == 0 ? (unsigned long long)valid_n : 0ull;
     flush_block<2, SPB>(counters, {cnt_rays, cnt_samples}, {mine, mine});
 }
@@ -1153,10 +1176,17 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     constexpr unsigned CS = YRT_SHADOW_BLOCK_CHUNK;
     __shared__ chunk_ring ring;
     chunk_ring_init<CS>(ring, B.queue + xcd);
+#ifdef YRT_TAIL_STATS
+    const unsigned long long tail_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned tail_items = 0;
+#endif
     for (;;) {
         const unsigned q = chunk_ring_next<CS>(ring, B.queue + xcd, lane);
         const unsigned it = xcd_item<C>(q, xcd, n_items);
         if (it >= n_items) break;
+#ifdef YRT_TAIL_STATS
+        tail_items++;
+#endif
         const int li = (int)(it % (unsigned)nl);
         const int bx = (int)(it / (unsigned)nl);
         // the light's frame and position: one wave-uniform record, through the scalar cache
@@ -1196,6 +1226,9 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         occ = lc == 0 ? false : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot);
         if (valid) B.occl[(size_t)li * B.capacity + idx] = occ ? 1 : 0;
     }
+#ifdef YRT_TAIL_STATS
+    tail_record(1, tail_t0, tail_items);
+#endif
     const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
     flush_block<1, SP_BLOCK>(counters, {cnt_shadow_rays}, {mine});
 }
@@ -1875,6 +1908,17 @@ extern "C" int yrt_debug_wide_stats(unsigned long long* out16, int reset) {
         (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_wide_stats), z, sizeof z);
     }
     return 0;
+}
+#endif
+
+#ifdef YRT_TAIL_STATS
+// out: 8192 x {start, end, items, xcd} for kernel k (0 k_primary_persist, 1 k_shadow_persist)
+extern "C" int yrt_debug_tail(unsigned long long* out, int k) {
+    if (k < 0 || k > 1) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(yrt::g_tail), sizeof(yrt::g_tail[0]), k * sizeof(yrt::g_tail[0])) ==
+                   hipSuccess
+               ? 0
+               : -1;
 }
 #endif
 
