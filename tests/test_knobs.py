@@ -4,7 +4,7 @@ The product is built with every knob at its default (yocto_raytracing_amd/build.
 The knobs that remain are either tunables with a measured default (register
 budgets, block sizes, XCD run lengths, the persistent-grid threshold) or kept
 variants the ledger refers to (LDS staging of the top 4-wide records, the north
-star's "hot node tiles in LDS") and the two diagnostic builds. None of them is
+star's "hot node tiles in LDS") and the three diagnostic builds. None of them is
 compiled by the normal build, so each non-default setting is compiled here for
 gfx950 (device code only) to keep it from rotting. A knob added to the sources
 without an entry below fails test_every_knob_is_listed.
@@ -26,6 +26,7 @@ VARIANTS = {
     "YRT_SHADOW_LDS_RECORDS": ["-DYRT_SHADOW_LDS_RECORDS=85"],
     "YRT_DEBUG_BOUNDS": ["-DYRT_DEBUG_BOUNDS"],
     "YRT_WIDE_STATS": ["-DYRT_WIDE_STATS"],
+    "YRT_TAIL_STATS": ["-DYRT_TAIL_STATS"],
     "YRT_TRACE_WAVES": ["-DYRT_TRACE_WAVES=7"],
     "YRT_SHADOW_WAVES": ["-DYRT_SHADOW_WAVES=6"],
     "YRT_SHADE_WAVES": ["-DYRT_SHADE_WAVES=5"],
@@ -45,7 +46,7 @@ VARIANTS = {
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],
     "YRT_PRIMARY_BLOCK": ["-DYRT_PRIMARY_BLOCK=256", "-DYRT_SHADOW_BLOCK=256", "-DYRT_SHADOW_BLOCK_CHUNK=64",
                           "-DYRT_SHADOW_LIGHT_MINOR=16", "-DYRT_XCD_CHUNK_PRIMARY=64",
-                          "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0", "-DYRT_PRIMARY_PERSIST_MIN_ITEMS=0",
+                          "-DYRT_SHADOW_PERSIST_MIN_ITEMS=0", "-DYRT_PRIMARY_PERSIST_MIN_ITEMS=1000000",
                           "-DYRT_PRIMARY_BLOCK_CHUNK=64"],
 }
 # knobs covered by another entry's defines
