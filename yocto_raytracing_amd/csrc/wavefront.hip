@@ -85,7 +85,7 @@ struct wf_buffers {
     __device__ __forceinline__ f4* rec1(int k) const { return rec1_ + (size_t)k * capacity; }
     int* count;             // level k >= 1, segment g: rays at count[(k * level_segments + g) * count_stride]
     int seg;                // slots per segment of a mirror level (seg_count)
-    unsigned* queue;        // per-XCD work counters of the persistent shadow kernel: [0, 8)
+    unsigned* queue;        // work counters of the persistent grids: shadow [0, 8) per XCD + [8] shared, primary [16, 24) + [24]
     const f4* trel;         // instance-level spine records relative to the camera origin
     int capacity;           // samples per chunk
     int nlevels;            // levels allocated
@@ -572,20 +572,49 @@ __global__ __launch_bounds__(WF_BLOCK) void k_relative_records(const f4* __restr
 // once every slot of the entry's previous chunk has been read (each taker reads its base
 // right after taking its slot, before it looks at the item, and slots are taken in
 // order, so every wait ends). All atomics are vector (lane 0) or LDS operations.
+#ifndef YRT_SHARED_TAIL
+// the persistent grids' last 1/YRT_SHARED_TAIL items come from one queue that every XCD
+// takes from once its own share is done (the XCDs' shares otherwise end up to 2 % of a
+// c4 launch apart, 6 % at a rank's share of an 8-way split: tools/tail_stats.py); 0: each
+// XCD keeps its static share to the end. A/B in one process (profiles/r4/ab_shared_tail):
+// 1/32 / 1/16 / 1/8 -- c4 24.67 -> 24.43 / 24.43 / 24.42 ms, rank 0 of 4 6.42 -> 6.34 /
+// 6.37 / 6.35, instance100k 32.92 -> 32.70 / 32.87 / 33.14 (its short any-hit grid pays
+// for a larger shared tail), rank 0 of 8 and c3 within 0.3 %
+#define YRT_SHARED_TAIL 32
+#endif
+constexpr unsigned tail_flag = 0x80000000u;  // a position in the shared tail
+constexpr unsigned gcd_u(unsigned a, unsigned b) { return b ? gcd_u(b, a % b) : a; }
+// items of the per-XCD head: whole super-runs of 8 x lcm(RUN, CS) (so that every XCD's
+// share is whole runs and whole block chunks); the rest is the shared tail
+template <unsigned RUN, unsigned CS>
+__device__ __forceinline__ unsigned head_items(unsigned n_items) {
+    constexpr unsigned G = 8u * (RUN / gcd_u(RUN, CS) * CS);
+    return YRT_SHARED_TAIL ? (n_items - n_items / YRT_SHARED_TAIL) / G * G : 0u;
+}
+// a block chunk's first position: from the XCD's own counter while its share lasts
+// (limit = positions per XCD), then from the shared one (flagged)
+template <unsigned CS>
+__device__ __forceinline__ unsigned chunk_fetch(unsigned* counter, unsigned* gcounter, unsigned limit) {
+    const unsigned k = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!YRT_SHARED_TAIL || k * CS + CS <= limit) return k * CS;
+    return tail_flag | __hip_atomic_fetch_add(gcounter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * CS;
+}
+
 struct chunk_ring {
     static constexpr unsigned R = 4;
     unsigned base[R], tag[R], reads[R], taken;
 };
 
 template <unsigned CS>
-__device__ __forceinline__ void chunk_ring_init(chunk_ring& ring, unsigned* counter) {
+__device__ __forceinline__ void chunk_ring_init(chunk_ring& ring, unsigned* counter, unsigned* gcounter = nullptr,
+                                                unsigned limit = ~0u) {
     static_assert(CS >= 2, "a chunk's middle slot fetches the next chunk");
     if (threadIdx.x < chunk_ring::R) {
         ring.tag[threadIdx.x] = threadIdx.x == 0 ? 0u : ~0u;
         ring.reads[threadIdx.x] = threadIdx.x == 0 ? 0u : CS;
     }
     if (threadIdx.x == 0) {
-        ring.base[0] = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * CS;
+        ring.base[0] = chunk_fetch<CS>(counter, gcounter, limit);
         ring.taken = 0;
     }
     __syncthreads();
@@ -593,7 +622,8 @@ __device__ __forceinline__ void chunk_ring_init(chunk_ring& ring, unsigned* coun
 
 // the calling wave's next position in its XCD's item sequence (wave-uniform)
 template <unsigned CS>
-__device__ __forceinline__ unsigned chunk_ring_next(chunk_ring& ring, unsigned* counter, unsigned lane) {
+__device__ __forceinline__ unsigned chunk_ring_next(chunk_ring& ring, unsigned* counter, unsigned lane,
+                                                    unsigned* gcounter = nullptr, unsigned limit = ~0u) {
     constexpr unsigned R = chunk_ring::R;
     unsigned t = 0;
     if (lane == 0) t = __hip_atomic_fetch_add(&ring.taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -602,8 +632,8 @@ __device__ __forceinline__ unsigned chunk_ring_next(chunk_ring& ring, unsigned* 
     if (o == CS / 2) {  // publish chunk g + 1
         const unsigned e1 = (g + 1) % R;
         unsigned nbase = 0;
-        if (lane == 0) nbase = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        nbase = (unsigned)__builtin_amdgcn_readfirstlane((int)nbase) * CS;
+        if (lane == 0) nbase = chunk_fetch<CS>(counter, gcounter, limit);
+        nbase = (unsigned)__builtin_amdgcn_readfirstlane((int)nbase);
         while (__hip_atomic_load(&ring.reads[e1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != CS)
             __builtin_amdgcn_s_sleep(1);
         if (lane == 0) {
@@ -627,6 +657,14 @@ __device__ __forceinline__ unsigned xcd_item(unsigned q, unsigned xcd, unsigned 
     const unsigned full = n_items / (8u * RUN) * (8u * RUN);
     const unsigned per_xcd = full / 8u;
     return q < per_xcd ? ((q / RUN) * 8u + xcd) * RUN + q % RUN : full + (q - per_xcd) * 8u + xcd;
+}
+// the same with a shared tail (YRT_SHARED_TAIL): an XCD's own positions cover whole runs of
+// the head, a flagged position is the tail's (head + its index; >= n_items: done)
+template <unsigned RUN>
+__device__ __forceinline__ unsigned split_item(unsigned q, unsigned xcd, unsigned n_items, unsigned head) {
+    if (!YRT_SHARED_TAIL) return xcd_item<RUN>(q, xcd, n_items);
+    if (q & tail_flag) return head + (q & ~tail_flag);
+    return ((q / RUN) * 8u + xcd) * RUN + q % RUN;
 }
 
 #ifdef YRT_TAIL_STATS
@@ -711,11 +749,13 @@ __global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_pri
     if (threadIdx.x == 0) A_lds = A, C_lds = C, B_lds = B;
     const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
-    unsigned* counter = B.queue + 8 + xcd;
-    chunk_ring_init<CS>(ring, counter);  // (its barrier also publishes the copies)
+    unsigned* counter = B.queue + 16 + xcd;
+    unsigned* gcounter = B.queue + 24;
+    const unsigned n_items = (unsigned)((C.npix * C.spp + 63) / 64);
+    const unsigned head = head_items<YRT_XCD_CHUNK_PRIMARY, CS>(n_items);
+    chunk_ring_init<CS>(ring, counter, gcounter, head / 8u);  // (its barrier also publishes the copies)
     tracer<false, false, true, SE, SPB> T;
     T.lane_stk = nullptr;
-    const unsigned n_items = (unsigned)((C.npix * C.spp + 63) / 64);
     work_counts wc;
     unsigned valid_n = 0;  // wave-uniform: camera samples of this wave
 #ifdef YRT_TAIL_STATS
@@ -723,8 +763,8 @@ __global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_pri
     unsigned tail_items = 0;
 #endif
     for (;;) {
-        const unsigned q = chunk_ring_next<CS>(ring, counter, lane);
-        const unsigned it = xcd_item<YRT_XCD_CHUNK_PRIMARY>(q, xcd, n_items);
+        const unsigned q = chunk_ring_next<CS>(ring, counter, lane, gcounter, head / 8u);
+        const unsigned it = split_item<YRT_XCD_CHUNK_PRIMARY>(q, xcd, n_items, head);
         if (it >= n_items) break;
 #ifdef YRT_TAIL_STATS
         tail_items++;
@@ -1214,14 +1254,15 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     // positions from the block's chunk ring (chunk_ring_next), YRT_SHADOW_BLOCK_CHUNK at a time
     constexpr unsigned CS = YRT_SHADOW_BLOCK_CHUNK;
     __shared__ chunk_ring ring;
-    chunk_ring_init<CS>(ring, B.queue + xcd);
+    const unsigned head = head_items<C, CS>(n_items);
+    chunk_ring_init<CS>(ring, B.queue + xcd, B.queue + 8, head / 8u);
 #ifdef YRT_TAIL_STATS
     const unsigned long long tail_t0 = __builtin_amdgcn_s_memrealtime();
     unsigned tail_items = 0;
 #endif
     for (;;) {
-        const unsigned q = chunk_ring_next<CS>(ring, B.queue + xcd, lane);
-        const unsigned it = xcd_item<C>(q, xcd, n_items);
+        const unsigned q = chunk_ring_next<CS>(ring, B.queue + xcd, lane, B.queue + 8, head / 8u);
+        const unsigned it = split_item<C>(q, xcd, n_items, head);
         if (it >= n_items) break;
 #ifdef YRT_TAIL_STATS
         tail_items++;
@@ -1575,7 +1616,7 @@ size_t camera_tiles(int cap, int spp) { return ((size_t)cap / (size_t)spp + TILE
 
 size_t workspace_bytes(int cap, int spp, int nlights, int nlevels) {
     size_t c = (size_t)cap;
-    size_t b = align_up(count_bytes(nlevels)) + align_up(16 * sizeof(unsigned)) + align_up(4 * sizeof(unsigned long long));
+    size_t b = align_up(count_bytes(nlevels)) + align_up(32 * sizeof(unsigned)) + align_up(4 * sizeof(unsigned long long));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
     if (YRT_SHADOW_BUNDLES) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
@@ -1600,7 +1641,7 @@ wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
         return (void*)q;
     };
     B.count = (int*)take(count_bytes(nlevels));
-    B.queue = (unsigned*)take(16 * sizeof(unsigned));
+    B.queue = (unsigned*)take(32 * sizeof(unsigned));
     B.lstats = (unsigned long long*)take(4 * sizeof(unsigned long long));
     B.surf0 = (f4*)take(16 * c);
     B.surf1 = (f4*)take(16 * c);
@@ -1793,7 +1834,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         if constexpr (!COUNT && PACKET) {
             persist = ((long long)nsamp + 63) / 64 >= (long long)YRT_PRIMARY_PERSIST_MIN_ITEMS;
             if (persist) {
-                hipError_t e = hipMemsetAsync(B.queue + 8, 0, 8 * sizeof(unsigned), stream);
+                hipError_t e = hipMemsetAsync(B.queue + 16, 0, 9 * sizeof(unsigned), stream);
                 if (e != hipSuccess) return e;
                 const int nb = ds.num_cus * (YRT_PRIMARY_WAVES * 4 * 64 / YRT_PRIMARY_SP_BLOCK);
                 if (B.cam_lists)
@@ -1847,7 +1888,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
                     {
-                        hipError_t e = hipMemsetAsync(B.queue, 0, 8 * sizeof(unsigned), stream);
+                        hipError_t e = hipMemsetAsync(B.queue, 0, 9 * sizeof(unsigned), stream);
                         if (e != hipSuccess) return e;
                     }
                     constexpr int L = YRT_SHADOW_LDS_RECORDS;
