@@ -161,3 +161,24 @@ def test_tile_lists_argument_errors(yrt):
 
     assert N.lib.yrt_scene_set_tile_lists(ds.handle, 3) == 1  # YRT_ERR_INVALID_ARG
     assert N.lib.yrt_scene_set_tile_lists(None, 0) == 1  # YRT_ERR_INVALID_ARG
+
+
+def test_lists_follow_the_view(yrt):
+    """one scene handle rendered from each of instance10000's five cameras in turn and back
+    to the first (`camera` selects scn->cameras[k]; the reference always takes the first,
+    raytrace.cpp:225): each new view is probed again, and every frame -- probed, forced on
+    or off -- equals the oracle's render from that camera"""
+    name, res, spp = "instance10000", 180, 4
+    ds = host(yrt, name).upload(0)
+    orc = Oracle(name)
+    for cam in (0, 1, 2, 3, 4, 0):
+        ref, n, _ = orc.render(res, spp, camera=cam)
+        imgs = []
+        for mode in ("auto", "on", "off"):
+            ds.set_tile_lists(mode)
+            img, st = yrt.raytrace(ds, (0.1, 0.1, 0.1), res, spp, camera=cam, return_stats=True)
+            assert st["rays"] == n
+            imgs.append(img)
+        for img in imgs[1:]:
+            np.testing.assert_array_equal(img.view(np.uint32), imgs[0].view(np.uint32))
+        check_oracle(imgs[0], ref, f"instance10000 camera {cam}")
