@@ -155,6 +155,12 @@ def test_lists_synthetic_lights(yrt, tmp_path, nlights, rotated, bundles):
 
 def test_tile_lists_argument_errors(yrt):
     ds = host(yrt, "instance1k").upload(0)
+    # a handle that has not rendered, and one whose renders never built lists, read back zeros
+    assert ds.tile_lists() == {"camera": False, "bundles": False, "camera_entries": 0, "camera_lists": 0,
+                               "bundle_entries": 0, "bundle_lists": 0}
+    ds.set_tile_lists("off")
+    yrt.raytrace(ds, (0.1, 0.1, 0.1), 90, 2)
+    assert ds.tile_lists()["camera"] is False and ds.tile_lists()["camera_lists"] == 0
     with pytest.raises(KeyError):
         ds.set_tile_lists("sometimes")
     from yocto_raytracing_amd import _native as N

@@ -412,7 +412,7 @@ int yrt_scene_tile_lists(yrt_scene* s, int* camera_on, int* bundles_on, unsigned
     return guarded([&] {
         yrt::device_scene& ds = *s->ds;
         hip_check(hipSetDevice(ds.device), "hipSetDevice");
-        if (ds.list_stats_ev) hip_check(hipEventSynchronize(ds.list_stats_ev), "list sums");
+        if (ds.list_stats_ev && ds.list_stats_recorded) hip_check(hipEventSynchronize(ds.list_stats_ev), "list sums");
         if (camera_on) *camera_on = ds.last_camera_lists;
         if (bundles_on) *bundles_on = ds.last_bundles;
         if (sums)

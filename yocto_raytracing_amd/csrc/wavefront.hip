@@ -1951,6 +1951,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                                       hipMemcpyDeviceToHost, stream);
         if (e == hipSuccess) e = hipEventRecord(ds.list_stats_ev, stream);
         if (e != hipSuccess) return e;
+        ds.list_stats_recorded = true;
     }
     return hipGetLastError();
 }

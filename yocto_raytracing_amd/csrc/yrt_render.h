@@ -73,6 +73,7 @@ struct device_scene {
     // drops each kind of list. Both ways give the same image.
     unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
     hipEvent_t list_stats_ev = nullptr;
+    bool list_stats_recorded = false;  // list_stats_ev has been recorded (yrt_scene_tile_lists waits on it)
     bool camera_lists_on = true, bundles_on = true;
     int lists_mode = 0;  // YRT_LISTS_AUTO (the above) / YRT_LISTS_ON / YRT_LISTS_OFF (yrt_scene_set_tile_lists)
     bool last_camera_lists = false, last_bundles = false;  // what the last render used
