@@ -1747,6 +1747,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     if (!ds.list_stats_host) {
         hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
         if (e != hipSuccess) return e;
+        memset(ds.list_stats_host, 0, 4 * sizeof(unsigned long long));
     }
     if (!ds.list_stats_ev) {
         hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
