@@ -154,7 +154,7 @@ def test_lists_synthetic_lights(yrt, tmp_path, nlights, rotated, bundles):
 
 
 def test_tile_lists_argument_errors(yrt):
-    ds = host(yrt, "instance1k").upload(0)
+    ds = yrt.DeviceScene(host(yrt, "instance1k"), 0)  # a handle of its own (upload() caches one)
     # a handle that has not rendered, and one whose renders never built lists, read back zeros
     assert ds.tile_lists() == {"camera": False, "bundles": False, "camera_entries": 0, "camera_lists": 0,
                                "bundle_entries": 0, "bundle_lists": 0}
