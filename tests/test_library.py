@@ -32,6 +32,16 @@ def test_exports_match_header(yrt):
     assert _native.lib.yrt_status_string(0) == b"ok"
 
 
+def test_null_handles_are_status_codes(yrt):
+    """the device-scene calls refuse a null handle with YRT_ERR_INVALID_ARG (no GPU needed)"""
+    from yocto_raytracing_amd import _native as N
+
+    lib = N.lib
+    assert lib.yrt_scene_set_tile_lists(None, 0) == 1
+    assert lib.yrt_scene_set_trace_algorithm(None, 0) == 1
+    assert lib.yrt_scene_tile_lists(None, None, None, None) == 1
+
+
 def test_render_params_defaults_mirror_cli(yrt):
     p = yrt.render_params()
     # main() defaults: -r 720, -s 1, -a 0.1 (raytrace.cpp:260-265)
