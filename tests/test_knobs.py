@@ -30,6 +30,7 @@ VARIANTS = {
     "YRT_NT_STREAMS": ["-DYRT_NT_STREAMS=0"],
     "YRT_SHARED_TAIL": ["-DYRT_SHARED_TAIL=0"],
     "YRT_BUNDLE_SORT": ["-DYRT_BUNDLE_SORT=1"],
+    "YRT_BUNDLE_SUPER": ["-DYRT_BUNDLE_SUPER=0"],
     "YRT_TRACE_WAVES": ["-DYRT_TRACE_WAVES=7"],
     "YRT_SHADOW_WAVES": ["-DYRT_SHADOW_WAVES=6"],
     "YRT_SHADE_WAVES": ["-DYRT_SHADE_WAVES=5"],

@@ -95,6 +95,7 @@ struct wf_buffers {
     f4* pbox;               // per 64-sample item: {lo.xyz, -1 if a hit point is not finite} {hi.xyz, -}
     int* lcount;            // per (bundle, light): candidate leaves, -1 = walk the tree
     f4* lists;              // per (bundle, light): bundle_recs wide records (wide_record_bytes each)
+    f4* slists;             // per (super-bundle, light): a leaf list (YRT_BUNDLE_SUPER)
     // camera lists (the closest hit of the camera rays, k_camera_lists)
     int cam_lists;          // 1: this chunk's camera rays walk their tile's list
     int* ccount;            // per 8x8-pixel tile of the chunk: listed leaves, -1 = walk the tree
@@ -894,63 +895,32 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     }
 }
 
-// one wave per (bundle, light): the candidate list (see above). Lane 16 s + k tests slot s of
-// the current wide record against sweep box k; the tree is walked with a lane-indexed stack.
-__global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffers B, int n_items) {
-    __shared__ float cand[4][bundle_max][8];  // per wave: lo.xyz, hi.xyz, word
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nl = S.nlights;
-    const int ngroups = (n_items + bundle_g - 1) / bundle_g;
-    const int gl = blockIdx.x * 4 + w;
-    if (gl >= ngroups * nl) return;  // (whole waves)
-    const int g = gl / nl, li = gl - g * nl;
-    // the bundle's box: lane l < bundle_g holds item g * bundle_g + l
-    float plx = INFINITY, ply = INFINITY, plz = INFINITY, phx = -INFINITY, phy = -INFINITY, phz = -INFINITY;
-    bool bad = false;
-    {
-        const int it = g * bundle_g + lane;
-        if (lane < bundle_g && it < n_items) {
-            const float4 a = ld4(B.pbox + 2 * it), b = ld4(B.pbox + 2 * it + 1);
-            plx = a.x, ply = a.y, plz = a.z, phx = b.x, phy = b.y, phz = b.z;
-            bad = a.w < 0.0f;
-        }
-    }
-    {
-        float lo[3] = {plx, ply, plz}, hi[3] = {phx, phy, phz};
-        wave_box(lo, hi);
-        plx = lo[0], ply = lo[1], plz = lo[2], phx = hi[0], phy = hi[1], phz = hi[2];
-    }
-    float4 lrec[5];
-    ld_records_at<5>(S.lights, (unsigned)(6 * li), lrec);
-    const bool ident = ubits(lrec[0].x) == 0x3f800000u && ubits(lrec[0].y) == 0 && ubits(lrec[0].z) == 0 &&
-                       ubits(lrec[1].x) == 0 && ubits(lrec[1].y) == 0x3f800000u && ubits(lrec[1].z) == 0 &&
-                       ubits(lrec[2].x) == 0 && ubits(lrec[2].y) == 0 && ubits(lrec[2].z) == 0x3f800000u;
-    const vec3f Lp = xyz(lrec[4]) + xyz(lrec[3]);
-    if (ballot(bad) || !ident || !(__builtin_isfinite(Lp.x) && __builtin_isfinite(Lp.y) && __builtin_isfinite(Lp.z))) {
-        if (lane == 0) B.lcount[gl] = -1;
-        return;
-    }
-    if (!(plx <= phx)) {  // no hit point in the bundle: no shadow ray
-        if (lane == 0) B.lcount[gl] = 0;
-        return;
-    }
+// The hull of box P = [P0, P1] and the point Lp, as the 16 lanes of a slot group hold it:
+// lane j = lane % 16, j == 0 the hull's box (P's box with Lp), j = 1..12 the plane through
+// Lp and box edge j - 1 of P when that edge is on P's silhouette seen from Lp (one adjacent
+// face turned towards Lp, the other away). A box is dropped only when some lane finds it
+// entirely outside its plane by more than the margin -- a conservative test (the hull's
+// other separating axes are not tried); every plane bounds the hull, so a hull holding more
+// rays (a super-bundle's) keeps everything a smaller one does.
+struct hull_t {
+    float bxl, bxh, byl, byh, bzl, bzh;   // j == 0
+    float nx, ny, nz, nd, nmargin;        // j >= 1 (nmargin infinite: no plane)
+    int j;
+};
+__device__ __forceinline__ hull_t make_hull(float plx, float ply, float plz, float phx, float phy, float phz, vec3f Lp,
+                                            int lane) {
+    hull_t H;
     const float M = fmaxf(fmaxf(fmaxf(fabsf(plx), fabsf(ply)), fmaxf(fabsf(plz), fabsf(phx))),
                           fmaxf(fmaxf(fabsf(phy), fabsf(phz)), fmaxf(fmaxf(fabsf(Lp.x), fabsf(Lp.y)), fabsf(Lp.z))));
     const float eps = 1e-3f + 3e-5f * M;
-    // The rays' hull: the convex hull of P and Lp. Lane j = lane % 16 of each slot's group
-    // holds one of its bounding planes: j == 0 the hull's box (P's box with Lp), j = 1..12 the
-    // plane through Lp and box edge j - 1 of P when that edge is on P's silhouette seen from
-    // Lp (one adjacent face turned towards Lp, the other away). A child box is dropped only
-    // when some lane finds it entirely outside its plane by more than the margin -- a
-    // conservative test (the hull's other separating axes are not tried).
-    const int j = lane & 15;
+    H.j = lane & 15;
     const float P0[3] = {plx, ply, plz}, P1[3] = {phx, phy, phz}, L3[3] = {Lp.x, Lp.y, Lp.z};
-    const float bxl = fminf(plx, Lp.x) - eps, bxh = fmaxf(phx, Lp.x) + eps;
-    const float byl = fminf(ply, Lp.y) - eps, byh = fmaxf(phy, Lp.y) + eps;
-    const float bzl = fminf(plz, Lp.z) - eps, bzh = fmaxf(phz, Lp.z) + eps;
-    float nx = 0.0f, ny = 0.0f, nz = 0.0f, nd = 0.0f, nmargin = INFINITY;
-    if (j >= 1 && j <= 12) {
-        const int e = j - 1, a = e >> 2, b = (a + 1) % 3, c = (a + 2) % 3;
+    H.bxl = fminf(plx, Lp.x) - eps, H.bxh = fmaxf(phx, Lp.x) + eps;
+    H.byl = fminf(ply, Lp.y) - eps, H.byh = fmaxf(phy, Lp.y) + eps;
+    H.bzl = fminf(plz, Lp.z) - eps, H.bzh = fmaxf(phz, Lp.z) + eps;
+    H.nx = 0.0f, H.ny = 0.0f, H.nz = 0.0f, H.nd = 0.0f, H.nmargin = INFINITY;
+    if (H.j >= 1 && H.j <= 12) {
+        const int e = H.j - 1, a = e >> 2, b = (a + 1) % 3, c = (a + 2) % 3;
         const bool bh = e & 1, ch = (e >> 1) & 1;  // the edge's sides on axes b and c
         // a face faces Lp when Lp lies strictly outside the box on that face's side
         const bool fb = bh ? L3[b] > P1[b] : L3[b] < P0[b];
@@ -962,36 +932,44 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
             e0[c] = e1[c] = ch ? P1[c] : P0[c];
             const float ux = e1[0] - e0[0], uy = e1[1] - e0[1], uz = e1[2] - e0[2];
             const float vx = L3[0] - e0[0], vy = L3[1] - e0[1], vz = L3[2] - e0[2];
-            nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
+            float nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
             // the box centre on the inner (negative) side
             const float cx = 0.5f * (P0[0] + P1[0]) - e0[0], cy = 0.5f * (P0[1] + P1[1]) - e0[1],
                         cz = 0.5f * (P0[2] + P1[2]) - e0[2];
             if (nx * cx + ny * cy + nz * cz > 0.0f) nx = -nx, ny = -ny, nz = -nz;
-            nd = nx * e0[0] + ny * e0[1] + nz * e0[2];
-            nmargin = (fabsf(nx) + fabsf(ny) + fabsf(nz)) * (eps + 1e-5f * M);
+            H.nx = nx, H.ny = ny, H.nz = nz;
+            H.nd = nx * e0[0] + ny * e0[1] + nz * e0[2];
+            H.nmargin = (fabsf(nx) + fabsf(ny) + fabsf(nz)) * (eps + 1e-5f * M);
         }
     }
+    return H;
+}
+// this lane's plane has the box entirely outside (a NaN bound never separates: the
+// reference's select-based slab test can pass a box with a NaN plane)
+__device__ __forceinline__ bool hull_sep(const hull_t& H, float clx, float cly, float clz, float chx, float chy,
+                                         float chz) {
+    if (H.j == 0) return clx > H.bxh || chx < H.bxl || cly > H.byh || chy < H.byl || clz > H.bzh || chz < H.bzl;
+    const float mn = H.nx * (H.nx > 0.0f ? clx : chx) + H.ny * (H.ny > 0.0f ? cly : chy) +
+                     H.nz * (H.nz > 0.0f ? clz : chz);
+    return mn - H.nd > H.nmargin;
+}
+// the instance-level leaves the hull does not exclude, from a walk of the any-hit tree (lane
+// 16 s + j tests slot s of the current wide record against plane j; a lane-indexed stack):
+// up to CAP of them into cand (lane 0 writes), else overflow
+template <int CAP>
+__device__ __forceinline__ void hull_walk(const dev_scene_view& S, const hull_t& H, int lane, float (*cand)[8], int& nc,
+                                          bool& overflow) {
     const int s = lane >> 4;  // the slot this lane tests
     const f4* wbase = sgpr_ptr(S.wnodes);
-    int stk = 0, sp = 0, nc = 0;
-    bool overflow = false;
+    int stk = 0, sp = 0;
+    nc = 0, overflow = false;
     uint32_t cur = (uint32_t)S.wtop_root;
     for (;;) {
         float4 r[7];
         ld_wide_record(wbase, cur, r);
         const float4 rs[7] = {r[0], r[1], r[2], r[3], r[4], r[5], r[6]};
         auto comp = [&](float4 v) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; };
-        const float clx = comp(rs[0]), cly = comp(rs[1]), clz = comp(rs[2]);
-        const float chx = comp(rs[3]), chy = comp(rs[4]), chz = comp(rs[5]);
-        // separated: entirely outside this lane's plane (a NaN bound never separates: the
-        // reference's select-based slab test can pass a box with a NaN plane)
-        bool sep;
-        if (j == 0) {
-            sep = clx > bxh || chx < bxl || cly > byh || chy < byl || clz > bzh || chz < bzl;
-        } else {
-            const float mn = nx * (nx > 0.0f ? clx : chx) + ny * (ny > 0.0f ? cly : chy) + nz * (nz > 0.0f ? clz : chz);
-            sep = mn - nd > nmargin;
-        }
+        const bool sep = hull_sep(H, comp(rs[0]), comp(rs[1]), comp(rs[2]), comp(rs[3]), comp(rs[4]), comp(rs[5]));
         const unsigned long long sm = ballot(sep);
         unsigned long long m = 0;
 #pragma unroll
@@ -999,25 +977,24 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
             const uint32_t wq = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
             if (wq != wide_leaf && !((sm >> (16 * q)) & 0xffffull)) m |= 0xffffull << (16 * q);
         }
-
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (!((m >> (16 * q)) & 0xffffull)) continue;
             const uint32_t word = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
             if (word & wide_leaf) {
-                if (nc == bundle_max) {
+                if (nc == CAP) {
                     overflow = true;
                     continue;
                 }
                 if (lane == 0) {
-                    const float4 c = {q == 0 ? r[0].x : q == 1 ? r[0].y : q == 2 ? r[0].z : r[0].w,
-                                      q == 0 ? r[1].x : q == 1 ? r[1].y : q == 2 ? r[1].z : r[1].w,
-                                      q == 0 ? r[2].x : q == 1 ? r[2].y : q == 2 ? r[2].z : r[2].w, 0};
-                    const float4 d = {q == 0 ? r[3].x : q == 1 ? r[3].y : q == 2 ? r[3].z : r[3].w,
-                                      q == 0 ? r[4].x : q == 1 ? r[4].y : q == 2 ? r[4].z : r[4].w,
-                                      q == 0 ? r[5].x : q == 1 ? r[5].y : q == 2 ? r[5].z : r[5].w, 0};
-                    float* e = cand[w][nc];
-                    e[0] = c.x, e[1] = c.y, e[2] = c.z, e[3] = d.x, e[4] = d.y, e[5] = d.z, e[6] = __uint_as_float(word);
+                    float* e = cand[nc];
+                    e[0] = q == 0 ? r[0].x : q == 1 ? r[0].y : q == 2 ? r[0].z : r[0].w;
+                    e[1] = q == 0 ? r[1].x : q == 1 ? r[1].y : q == 2 ? r[1].z : r[1].w;
+                    e[2] = q == 0 ? r[2].x : q == 1 ? r[2].y : q == 2 ? r[2].z : r[2].w;
+                    e[3] = q == 0 ? r[3].x : q == 1 ? r[3].y : q == 2 ? r[3].z : r[3].w;
+                    e[4] = q == 0 ? r[4].x : q == 1 ? r[4].y : q == 2 ? r[4].z : r[4].w;
+                    e[5] = q == 0 ? r[5].x : q == 1 ? r[5].y : q == 2 ? r[5].z : r[5].w;
+                    e[6] = __uint_as_float(word);
                 }
                 nc++;
             } else {
@@ -1029,11 +1006,147 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         sp--;
         cur = (uint32_t)__builtin_amdgcn_readlane(stk, sp);
     }
+}
+
+// the box of the hit points of items [i0, i0 + n) (n <= 4 * 64: each lane takes up to four),
+// whether any is not finite, and the light's position if its frame is the identity
+__device__ __forceinline__ void bundle_box(const wf_buffers& B, int i0, int n, int n_items, int lane, float& plx,
+                                           float& ply, float& plz, float& phx, float& phy, float& phz, bool& bad) {
+    plx = ply = plz = INFINITY, phx = phy = phz = -INFINITY;
+    bad = false;
+    for (int k = 0; k < 4; k++) {
+        const int o = k * 64 + lane, it = i0 + o;
+        if (o < n && it < n_items) {
+            const float4 a = ld4(B.pbox + 2 * it), b = ld4(B.pbox + 2 * it + 1);
+            plx = fminf(plx, a.x), ply = fminf(ply, a.y), plz = fminf(plz, a.z);
+            phx = fmaxf(phx, b.x), phy = fmaxf(phy, b.y), phz = fmaxf(phz, b.z);
+            bad = bad || a.w < 0.0f;
+        }
+    }
+    float lo[3] = {plx, ply, plz}, hi[3] = {phx, phy, phz};
+    wave_box(lo, hi);
+    plx = lo[0], ply = lo[1], plz = lo[2], phx = hi[0], phy = hi[1], phz = hi[2];
+}
+__device__ __forceinline__ bool light_position(const dev_scene_view& S, int li, vec3f& Lp) {
+    float4 lrec[5];
+    ld_records_at<5>(S.lights, (unsigned)(6 * li), lrec);
+    const bool ident = ubits(lrec[0].x) == 0x3f800000u && ubits(lrec[0].y) == 0 && ubits(lrec[0].z) == 0 &&
+                       ubits(lrec[1].x) == 0 && ubits(lrec[1].y) == 0x3f800000u && ubits(lrec[1].z) == 0 &&
+                       ubits(lrec[2].x) == 0 && ubits(lrec[2].y) == 0 && ubits(lrec[2].z) == 0x3f800000u;
+    Lp = xyz(lrec[4]) + xyz(lrec[3]);
+    return ident && __builtin_isfinite(Lp.x) && __builtin_isfinite(Lp.y) && __builtin_isfinite(Lp.z);
+}
+
+#ifndef YRT_BUNDLE_SUPER
+// two-level build: one tree walk per (super-bundle of 4 consecutive bundles, light) into a
+// list of up to super_max leaves, which each bundle then filters with its own planes
+// instead of walking the tree (a super list that overflows: the bundles walk). A/B in one
+// process (profiles/r4/ab_bundle_super): the lists phase at c4 0.28 -> 0.24 ms, c5 rank 0
+// of 8 0.82 -> 0.67 ms; identical images
+#define YRT_BUNDLE_SUPER 1
+#endif
+constexpr int super_bundles = 4;
+constexpr int super_max = 32;
+constexpr int super_list_f4 = 1 + 2 * super_max;  // {count} then {lo, word} {hi, 0} per leaf
+
+// one wave per (super-bundle, light): its list at B.slists
+__global__ __launch_bounds__(256) void k_bundle_super(dev_scene_view S, wf_buffers B, int n_items) {
+    __shared__ float cand[4][super_max][8];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nl = S.nlights;
+    const int nsuper = (n_items + super_bundles * bundle_g - 1) / (super_bundles * bundle_g);
+    const int sl = blockIdx.x * 4 + w;
+    if (sl >= nsuper * nl) return;  // (whole waves)
+    const int sg = sl / nl, li = sl - sg * nl;
+    f4* out = B.slists + (size_t)sl * super_list_f4;
+    float plx, ply, plz, phx, phy, phz;
+    bool bad;
+    bundle_box(B, sg * super_bundles * bundle_g, super_bundles * bundle_g, n_items, lane, plx, ply, plz, phx, phy, phz,
+               bad);
+    vec3f Lp;
+    const bool lok = light_position(S, li, Lp);
+    int nc = -1;
+    if (!ballot(bad) && lok) {
+        if (!(plx <= phx)) {
+            nc = 0;
+        } else {
+            const hull_t H = make_hull(plx, ply, plz, phx, phy, phz, Lp, lane);
+            bool overflow;
+            hull_walk<super_max>(S, H, lane, cand[w], nc, overflow);
+            if (overflow) nc = -1;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's candidate stores
+    if (lane < 2 * max(nc, 0)) {
+        const float* e = cand[w][lane >> 1];
+        reinterpret_cast<float4*>(out)[1 + lane] =
+            (lane & 1) ? float4{e[3], e[4], e[5], 0.0f} : float4{e[0], e[1], e[2], e[6]};
+    }
+    if (lane == 0) reinterpret_cast<float4*>(out)[0] = float4{__int_as_float(nc), 0.0f, 0.0f, 0.0f};
+}
+
+// one wave per (bundle, light): the candidate list (see above) -- from the super-bundle's
+// list (YRT_BUNDLE_SUPER) or a walk of the tree -- as a chain of wide records
+__global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffers B, int n_items) {
+    __shared__ float cand[4][bundle_max][8];  // per wave: lo.xyz, hi.xyz, word
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nl = S.nlights;
+    const int ngroups = (n_items + bundle_g - 1) / bundle_g;
+    const int gl = blockIdx.x * 4 + w;
+    if (gl >= ngroups * nl) return;  // (whole waves)
+    const int g = gl / nl, li = gl - g * nl;
+    float plx, ply, plz, phx, phy, phz;
+    bool bad;
+    bundle_box(B, g * bundle_g, bundle_g, n_items, lane, plx, ply, plz, phx, phy, phz, bad);
+    vec3f Lp;
+    if (ballot(bad) || !light_position(S, li, Lp)) {
+        if (lane == 0) B.lcount[gl] = -1;
+        return;
+    }
+    if (!(plx <= phx)) {  // no hit point in the bundle: no shadow ray
+        if (lane == 0) B.lcount[gl] = 0;
+        return;
+    }
+    const hull_t H = make_hull(plx, ply, plz, phx, phy, phz, Lp, lane);
+    int nc = 0;
+    bool overflow = false;
+    int sc = -1;  // the super-bundle's list length, -1: walk the tree
+    const f4* sup = nullptr;
+    if (YRT_BUNDLE_SUPER && bundle_g * super_bundles <= 256) {
+        sup = B.slists + (size_t)((g / super_bundles) * nl + li) * super_list_f4;
+        sc = __builtin_amdgcn_readfirstlane(__float_as_int(ld4(sup).x));
+    }
+    if (sc >= 0) {
+        // the super list's leaves that this bundle's own planes do not exclude: lane 16 s + j
+        // tests leaf c0 + s against plane j, four leaves a pass
+        for (int c0 = 0; c0 < sc && !overflow; c0 += 4) {
+            const int e = c0 + (lane >> 4);
+            float4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+            if (e < sc) a = ld4(sup + 1 + 2 * e), b = ld4(sup + 2 + 2 * e);
+            const bool sep = e >= sc || hull_sep(H, a.x, a.y, a.z, b.x, b.y, b.z);
+            const unsigned long long sm = ballot(sep);
+            unsigned keep = 0;  // bit q: leaf c0 + q stays
+            for (int q = 0; q < 4; q++) keep |= ((sm >> (16 * q)) & 0xffffull) ? 0u : 1u << q;
+            const int k = __popc(keep);
+            if (nc + k > bundle_max) {
+                overflow = true;
+                break;
+            }
+            const int q = lane >> 4;
+            if ((lane & 15) == 0 && ((keep >> q) & 1u)) {
+                float* d = cand[w][nc + __popc(keep & ((1u << q) - 1u))];
+                d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = b.x, d[4] = b.y, d[5] = b.z, d[6] = a.w;
+            }
+            nc += k;
+        }
+    } else {
+        hull_walk<bundle_max>(S, H, lane, cand[w], nc, overflow);
+    }
     if (overflow) {
         if (lane == 0) B.lcount[gl] = -1;
         return;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's candidate stores, before any lane reads them
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the candidate stores, before any lane reads them
     if (YRT_BUNDLE_SORT && nc > 1) {
         // the leaves in the order the bundle's rays meet them (box centres projected on the
         // direction from the hit points to the light; YRT_BUNDLE_SORT), so that the chain's
@@ -1643,6 +1756,7 @@ size_t count_bytes(int nlevels) { return sizeof(int) * ((size_t)nlevels + 1) * l
 size_t bundle_items(int cap) { return ((size_t)cap + 63) / 64; }
 size_t bundle_count(int cap) { return (bundle_items(cap) + bundle_g - 1) / bundle_g; }
 int bundle_lights(int nlights) { return nlights <= bundle_max_lights ? nlights : 0; }
+size_t super_count(int cap) { return (bundle_count(cap) + super_bundles - 1) / super_bundles; }
 
 // camera lists: 8x8-pixel tiles of a chunk of cap samples at spp samples per pixel
 size_t camera_tiles(int cap, int spp) { return ((size_t)cap / (size_t)spp + TILE * TILE - 1) / (TILE * TILE); }
@@ -1654,6 +1768,7 @@ size_t workspace_bytes(int cap, int spp, int nlights, int nlevels) {
     if (YRT_SHADOW_BUNDLES) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
         b += align_up(32 * bundle_items(cap)) + align_up(4 * gl) + align_up((size_t)bundle_recs * wide_record_bytes * gl);
+        if (YRT_BUNDLE_SUPER) b += align_up(super_count(cap) * bundle_lights(nlights) * super_list_f4 * 16);
     }
     if (YRT_CAMERA_LISTS) {
         const size_t nt = camera_tiles(cap, spp);
@@ -1686,6 +1801,7 @@ wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
         B.pbox = (f4*)take(32 * bundle_items(cap));
         B.lcount = (int*)take(4 * gl);
         B.lists = (f4*)take((size_t)bundle_recs * wide_record_bytes * gl);
+        if (YRT_BUNDLE_SUPER) B.slists = (f4*)take(super_count(cap) * bundle_lights(nlights) * super_list_f4 * 16);
     }
     if (YRT_CAMERA_LISTS) {
         const size_t nt = camera_tiles(cap, spp);
@@ -1910,6 +2026,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 if (level == 0 && shadow_persist && B.bundles) {  // the bundles' candidate lists
                     t = T.begin(phase_lists, stream);
+                    if (YRT_BUNDLE_SUPER) {
+                        const long long ns = (long long)super_count(nsamp) * ds.nlights;
+                        hipLaunchKernelGGL(k_bundle_super, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, stream, ds.view,
+                                           B, tgrid);
+                    }
                     const long long nw = (long long)bundle_count(nsamp) * ds.nlights;
                     hipLaunchKernelGGL(k_bundle_lists, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream, ds.view, B,
                                        tgrid);
