@@ -197,8 +197,9 @@ int yrt_scene_set_trace_algorithm(yrt_scene* ds, int algorithm);
 /* per-tile candidate lists of yrt_render (camera lists and shadow
  * bundles; identical images either way): YRT_LISTS_AUTO (default) probes each new view and
  * keeps the lists while they average <= 6 leaves, YRT_LISTS_ON builds them whenever the
- * scene allows (an instance tree of >= 8 wide records, unrotated point lights), YRT_LISTS_OFF
- * never builds them */
+ * scene allows (an instance tree of >= 8 wide records; shadow bundles for at most 8 lights,
+ * a rotated light's rays walking the tree), YRT_LISTS_OFF never builds them. Set it
+ * between renders of the handle, not while one is in flight. */
 int yrt_scene_set_tile_lists(yrt_scene* ds, int mode);
 /* the lists' state after the last yrt_render on this handle (synchronises with it):
  * whether each kind is in use, and sums[4] = {camera-list entries, camera lists, bundle-list
