@@ -1,0 +1,7 @@
+set -u
+OUT=gpurun_out/final
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; tail -n 2 $OUT/pytest.log; if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+rc=$?; tail -n 1 $OUT/smoke.log; exit $rc
