@@ -188,3 +188,4 @@ def test_lists_follow_the_view(yrt):
         for img in imgs[1:]:
             np.testing.assert_array_equal(img.view(np.uint32), imgs[0].view(np.uint32))
         check_oracle(imgs[0], ref, f"instance10000 camera {cam}")
+

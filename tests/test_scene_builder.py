@@ -70,3 +70,21 @@ def test_synthetic_fixture_is_reproducible(yrt, tmp_path):
     build_scene(out)
     assert gzip.open(out).read() == gzip.open(scene_path("lines")).read()
     assert hashlib.sha256(gzip.open(out).read()).hexdigest() == digests()["lines"]["scene_sha256"]
+
+
+def test_nan_bounded_instance_is_refused_by_the_build(yrt):
+    """An instance whose box carries a NaN (a shape whose root box keeps a NaN vertex: the
+    reference's ?: folds keep a NaN that comes last) makes the instance level's centroid box
+    NaN, every midpoint comparison false and the split empty: the reference's make_node then
+    recurses forever (scene.cpp:572-603, its assert compiled out); the build refuses it. So no
+    buildable scene has a NaN-bounded instance-level leaf, and the candidate lists never list
+    one (wavefront.hip k_bundle_lists still folds a chain box NaN-sticky, so a NaN bound could
+    only widen it)."""
+    s, m, tri = tiny(yrt)
+    bad = s.add_shape(np.array([[0, 0.2, 0], [0.3, 0.2, 0], [0.1, np.nan, 0.1]], np.float32),
+                      norm=[[0, 1, 0]] * 3, texcoord=[[0, 0]] * 3, triangles=[[0, 1, 2]])
+    for k in range(8):
+        s.add_instance(np.r_[1, 0, 0, 0, 1, 0, 0, 0, 1, k, 0, 0].astype(np.float32), tri, m)
+    s.add_instance(np.r_[1, 0, 0, 0, 1, 0, 0, 0, 1, 3, 0, 1].astype(np.float32), bad, m)
+    with pytest.raises(yrt.YrtError, match="degenerate centroids"):
+        yrt.build_bvh(s)

@@ -47,3 +47,33 @@ def code_identity(path) -> str:
     for co in code_objects(Path(path)):
         h.update(hashlib.sha256(co).digest())
     return h.hexdigest()
+
+
+_RES_KEYS = {"vgpr_count": "vgpr", "sgpr_count": "sgpr", "vgpr_spill_count": "vgpr_spill",
+             "sgpr_spill_count": "sgpr_spill", "private_segment_fixed_size": "private",
+             "group_segment_fixed_size": "lds", "max_flat_workgroup_size": "block"}
+
+
+def kernel_resources(path) -> dict:
+    """per kernel symbol of the gfx950 code objects in `path`: its register counts, spills,
+    private (scratch) bytes per lane and static LDS bytes, from the code object's
+    AMDHSA metadata note (llvm-readelf --notes)"""
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for k, co in enumerate(code_objects(Path(path))):
+            p = Path(td) / f"co{k}"
+            p.write_bytes(co)
+            notes = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(p)], check=True,
+                                   capture_output=True, text=True).stdout
+            # one YAML mapping per kernel under amdhsa.kernels, each starting with "  - ."
+            for block in re.split(r"\n  - (?=\.)", notes)[1:]:
+                m = re.search(r"^\s*\.name:\s+(\S+)", block, re.M)
+                if not m:
+                    continue
+                res = {}
+                for key, short in _RES_KEYS.items():
+                    v = re.search(rf"^\s*\.{key}:\s+(\d+)", block, re.M)
+                    if v:
+                        res[short] = int(v.group(1))
+                out[m.group(1)] = res
+    return out

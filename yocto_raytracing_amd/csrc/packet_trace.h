@@ -455,7 +455,13 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
     return false;
 }
 
-constexpr int packet_block = 256;  // >= threads per block of every kernel that runs packet_first
+constexpr int packet_block = 256;
+#ifndef YRT_R5_LANE
+#define YRT_R5_LANE 1
+#endif
+#ifndef YRT_R5_UORIG
+#define YRT_R5_UORIG 1
+#endif  // >= threads per block of every kernel that runs packet_first
 
 
 // one descent of the closest-hit walk from the spine record at byte offset `node` of
@@ -562,7 +568,7 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
 // leaf that fails, it either never reaches or tests and fails. Entries {lo - o, first}
 // {hi - o, count} (32 bytes).
 template <int OCT>
-__device__ __forceinline__ unsigned long long list_leaf_test(vec3f ci, float tmin, float tmax, const float4 (&e)[2],
+__device__ __forceinline__ unsigned long long list_entry_test(vec3f ci, float tmin, float tmax, const float4 (&e)[2],
                                                              unsigned long long lanes) {
     return ballot(box_oct<OCT>(vec3f{0.0f, 0.0f, 0.0f}, ci, tmin, tmax, e[0].x, e[0].y, e[0].z, e[1].x, e[1].y,
                                e[1].z)) &
@@ -575,17 +581,31 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                                              const float4* lds = nullptr, const f4* lbase = nullptr,
                                              int ln = -1) {
     static_assert(spine_len == 2, "packet_first walks two-node spine records");
-    const unsigned long long me = 1ull << __lane_id();
+    // (this lane's bit, wave-relative LDS slot: recomputed where used -- lane_now() is not
+    // hoisted out of a persistent caller's item loop, where a held copy would be spilled)
+    const unsigned long long me = (COUNT || !YRT_R5_LANE) ? 1ull << __lane_id() : 0ull;
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
-    const vec3f wo = wray.o, wd = wray.d;
+    // REL: every live lane's ray starts at the one origin the records were made relative to
+    // (the camera's): it is read from the first live lane into SGPRs, so the walk holds no
+    // VGPRs for it
+    const int fl = __builtin_ctzll(live);
+    const vec3f wo = (REL && YRT_R5_UORIG) ? vec3f{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(wray.o.x), fl)),
+                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wray.o.y), fl)),
+                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wray.o.z), fl))}
+                         : wray.o;
+    const vec3f wd = wray.d;
     const float tmin = wray.tmin;
     float tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = rcp3(wd, live);
     // the world inverse direction, parked in LDS for the returns from instance leaves
     // (three ds_read instead of three IEEE divisions; three VGPRs stay free)
     __shared__ float wi_lds[3][BS];
-    wi_lds[0][threadIdx.x] = ci.x, wi_lds[1][threadIdx.x] = ci.y, wi_lds[2][threadIdx.x] = ci.z;
+    const int wave = uniform((int)threadIdx.x >> 6);
+    {
+        const int t = YRT_R5_LANE ? wave * 64 + lane_now() : (int)threadIdx.x;
+        wi_lds[0][t] = ci.x, wi_lds[1][t] = ci.y, wi_lds[2][t] = ci.z;
+    }
     float hw1 = 0, hw2 = 0;
     int hslot = -1, hei = -1;
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
@@ -603,52 +623,76 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     vec3f icd, ici;
     enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
     const int ioct = wave_octant(ici, live);
-    const bool list = LIST && REL && !COUNT && ln >= 0;
-    // list mode: the list's address, length and next entry are parked in this wave's LDS
-    // slot between list steps, so they hold no registers through the instance walks
+    // list mode (LIST, REL): level 0 is driven by the tile's frontier list (k_camera_lists):
+    // its address, length and next entry are parked in this wave's LDS slot between list
+    // steps, so they hold no registers through the walk; a wave without a list (ln < 0) walks
+    // the tree from its root as the list's one virtual entry
+    constexpr bool LM = LIST && REL && !COUNT;
     __shared__ int list_lds[BS / 64][4];
-    int* const lst = list_lds[threadIdx.x >> 6];
-    if (list) {
+    int* const lst = list_lds[wave];
+    if constexpr (LM) {
         lst[0] = (int)(unsigned)(unsigned long long)lbase, lst[1] = (int)((unsigned long long)lbase >> 32);
         lst[2] = ln, lst[3] = 0;
     }
+    bool lstep = LM;  // the next step takes the next list entry (the walk's first step, in list mode)
     for (;;) {
         uint32_t lcl = 0;
-        if (list && level == 0) {
-            // ---- list mode: the next leaf some live lane passes, or the end ----
+        bool descend = true;
+        if (LM && lstep) {
+            // ---- list step: the next entry some live lane passes, or the end of the walk ----
+            lstep = false;
             mask = 0;
             asm volatile("" ::: "memory");
-            const f4* lb = (const f4*)((unsigned long long)(unsigned)uniform(lst[1]) << 32 | (unsigned)uniform(lst[0]));
             const int lend = uniform(lst[2]);
             int lnext = uniform(lst[3]);
-            while (lnext < lend) {
-                float4 e[2];
-                ld_records_at<2>(lb, (unsigned)(2 * lnext), e);
-                lnext++;
-                const unsigned long long lanes = live & ~done;
-                unsigned long long m;
-                switch (oct) {
-                    case 0: m = list_leaf_test<0>(ci, tmin, tmax, e, lanes); break;
-                    case 1: m = list_leaf_test<1>(ci, tmin, tmax, e, lanes); break;
-                    case 2: m = list_leaf_test<2>(ci, tmin, tmax, e, lanes); break;
-                    case 3: m = list_leaf_test<3>(ci, tmin, tmax, e, lanes); break;
-                    case 4: m = list_leaf_test<4>(ci, tmin, tmax, e, lanes); break;
-                    case 5: m = list_leaf_test<5>(ci, tmin, tmax, e, lanes); break;
-                    case 6: m = list_leaf_test<6>(ci, tmin, tmax, e, lanes); break;
-                    case 7: m = list_leaf_test<7>(ci, tmin, tmax, e, lanes); break;
-                    default: m = list_leaf_test<8>(ci, tmin, tmax, e, lanes); break;
-                }
-                if (m) {
-                    node = uniform(ibits(e[0].w));
-                    lcl = (uint32_t)uniform(ibits(e[1].w)) | leaf_bit;
-                    mask = m;
-                    break;
+            if (lend < 0) {
+                if (lnext == 0) node = 0, mask = live & ~done, lnext = 1;  // the root's record
+            } else {
+                const f4* lb =
+                    (const f4*)((unsigned long long)(unsigned)uniform(lst[1]) << 32 | (unsigned)uniform(lst[0]));
+                while (lnext < lend) {
+                    float4 e[2];
+                    ld_records_at<2>(lb, (unsigned)(2 * lnext), e);
+                    lnext++;
+                    const unsigned long long lanes = live & ~done;
+                    unsigned long long m;
+                    switch (oct) {
+                        case 0: m = list_entry_test<0>(ci, tmin, tmax, e, lanes); break;
+                        case 1: m = list_entry_test<1>(ci, tmin, tmax, e, lanes); break;
+                        case 2: m = list_entry_test<2>(ci, tmin, tmax, e, lanes); break;
+                        case 3: m = list_entry_test<3>(ci, tmin, tmax, e, lanes); break;
+                        case 4: m = list_entry_test<4>(ci, tmin, tmax, e, lanes); break;
+                        case 5: m = list_entry_test<5>(ci, tmin, tmax, e, lanes); break;
+                        case 6: m = list_entry_test<6>(ci, tmin, tmax, e, lanes); break;
+                        case 7: m = list_entry_test<7>(ci, tmin, tmax, e, lanes); break;
+                        default: m = list_entry_test<8>(ci, tmin, tmax, e, lanes); break;
+                    }
+                    if (m) {
+                        const int w0 = uniform(ibits(e[0].w));
+                        const uint32_t w1 = (uint32_t)uniform(ibits(e[1].w));
+                        mask = m;
+                        if (w1 & leaf_bit) {  // an instance-level leaf: its instances next
+                            node = w0, lcl = w1;
+                            descend = false;
+                        } else {
+                            // a subtree root X that the lanes of m pass: what first_descend does
+                            // once X passes -- push X's child start (record w0) for them and go on
+                            // at child start+1, whose record follows start's
+                            stk_node = writelane(stk_node, w0, sp);
+                            stk_mlo = writelane(stk_mlo, (int)(uint32_t)m, sp);
+                            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m >> 32), sp);
+                            sp++;
+                            node = w0 + spine_record_bytes;
+                        }
+                        break;
+                    }
                 }
             }
             if (!mask) break;
             lst[3] = lnext;
             asm volatile("" ::: "memory");
-        } else {
+        }
+        if (descend) {
         // ---- descent: one spine record per step, until a leaf or no passing lane ----
         DBG_CHECK(node >= 0 && (node % spine_record_bytes) == 0 && sp >= 0 && sp < 63 &&
                       (level == 0 ? node / spine_record_bytes < S.ntnodes
@@ -696,7 +740,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 level = 1;
                 base = sp;
             } else {
-                const bool in = (lmask & me) != 0;
+                const bool in = YRT_R5_LANE ? ((lmask >> lane_now()) & 1ull) != 0 : (lmask & me) != 0;
                 int leaf_hit = 0;
                 DBG_CHECK(lstart >= 0 && lstart + lcount <= S.nsprims, 2, lstart, lcount, level, kind, sp);
                 if (kind == kind_triangles) {
@@ -777,9 +821,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 pbase = ptop;
                 co = wo;
                 cd = wd;
-                ci = {wi_lds[0][threadIdx.x], wi_lds[1][threadIdx.x], wi_lds[2][threadIdx.x]};
+                {
+                    const int t = YRT_R5_LANE ? wave * 64 + lane_now() : (int)threadIdx.x;
+                    ci = {wi_lds[0][t], wi_lds[1][t], wi_lds[2][t]};
+                }
                 oct = woct;
-                if (list) break;  // the next list entry (level 0 of list mode has no stack)
             }
             if (sp == 0) {
                 finished = true;
@@ -792,7 +838,10 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                    ~done;
             if (mask) break;
         }
-        if (finished) break;
+        if (finished) {
+            if (!LM) break;
+            lstep = true;  // this list entry is done: the next one
+        }
     }
     if (hslot < 0) return false;
     hr.slot = hslot;

@@ -191,6 +191,19 @@ typedef float gvec4 __attribute__((ext_vector_type(4)));
 // -0.6 to -0.8 %, identical images)
 #define YRT_NT_STREAMS 1
 #endif
+// a constant made where it is used: v_mov of the immediate in volatile asm, which the compiler
+// does not hoist out of a persistent kernel's item loop (a hoisted {0, 0, 0, -1} register
+// tuple is held across the walk and spilled: the tuple is not rematerialised)
+#ifndef YRT_R5_VCONST
+#define YRT_R5_VCONST 1
+#endif
+template <int IMM>
+__device__ __forceinline__ float vconst() {
+    if (!YRT_R5_VCONST) return __int_as_float(IMM);
+    float r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "n"(IMM));
+    return r;
+}
 __device__ __forceinline__ void gstore(f4* p, int idx, float x, float y, float z, float w) {
     auto* q = (__attribute__((address_space(1))) gvec4*)p + idx;
     if (YRT_NT_STREAMS)
@@ -244,7 +257,7 @@ __device__ __forceinline__ void store_not_sample(const wf_buffers& B, int idx) {
     if (YRT_HIT16)
         gstore(B.surf0, idx, __int_as_float(-2), 0, 0, 0);
     else
-        gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-2));
+        gstore(B.surf0, idx, vconst<0>(), vconst<0>(), vconst<0>(), vconst<-2>());
 }
 // a HIT16 record's surface (eval_pos/eval_norm/eval_texcoord, scene.h:159-218); ew.x is
 // rebuilt as packet_first builds it (1 - w1 - w2, the same bits)
@@ -258,15 +271,23 @@ __device__ __forceinline__ void store_hit16(const wf_buffers& B, int idx, bool h
         gstore(B.surf0, idx, __int_as_float(hr.slot), __int_as_float(hr.ei), hr.ew.y, hr.ew.z);
 }
 
-__device__ __forceinline__ void store_surface(const wf_buffers& B, int idx, bool hit, const surface& sf) {
+// The surface record of a sample: the hit's surface is evaluated and stored on the hit lanes
+// only, and a miss stores its marker. (Written as `surface sf = {}; if (hit) sf = ...;` the
+// conditional aggregate copy kept the first 28 bytes of sf in a private array, which the
+// backend promoted to 28 KB of LDS per 1024-thread block; its 64-bit address then took
+// VGPRs the closest-hit walk spilled to scratch.)
+__device__ __forceinline__ vec3f store_hit_surface(const dev_scene_view& S, const wf_buffers& B, int idx, bool hit,
+                                                   const hit_record& hr) {
     if (!hit) {
-        gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-1));
-        return;
+        gstore(B.surf0, idx, vconst<0>(), vconst<0>(), vconst<0>(), vconst<-1>());
+        return {0, 0, 0};
     }
+    const surface sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
     gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind));
     gstore(B.surf1, idx, sf.n.x, sf.n.y, sf.n.z, sf.uv.x);
     // uv is read only by texture lookups: a scene without textures never needs it
     if (!YRT_SKIP_UNUSED_V || B.need_v) gstore(B.surfv, idx, sf.uv.y);
+    return sf.p;
 }
 
 // the two traversal schedules behind one call: PACKET = wave-coherent walk
@@ -493,6 +514,9 @@ __device__ __forceinline__ void store_item_box(const wf_buffers& B, int idx, boo
     }
 }
 
+#ifndef YRT_R5_SURF
+#define YRT_R5_SURF 1
+#endif
 #ifndef YRT_PRIMARY_REL
 #define YRT_PRIMARY_REL 1  // camera rays walk the instance level on camera-relative records
 #endif
@@ -548,10 +572,18 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
         if (YRT_HIT16) {
             store_hit16(B, idx, hit, hr);
             if (YRT_SHADOW_BUNDLES && hit && B.bundles) hp = eval_surface(S, hr.slot, hr.ei, hr.ew).p;
+        } else if (YRT_R5_SURF) {
+            hp = store_hit_surface(S, B, idx, hit, hr);
         } else {
             surface sf = {};
             if (hit) sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
-            store_surface(B, idx, hit, sf);
+            if (!hit)
+                gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-1));
+            else {
+                gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind));
+                gstore(B.surf1, idx, sf.n.x, sf.n.y, sf.n.z, sf.uv.x);
+                if (!YRT_SKIP_UNUSED_V || B.need_v) gstore(B.surfv, idx, sf.uv.y);
+            }
             hp = sf.p;
         }
     }
@@ -734,6 +766,9 @@ static_assert((YRT_PRIMARY_WAVES * 4 * 64) % YRT_PRIMARY_SP_BLOCK == 0, "whole b
 // instead: 62 SGPR and 12 VGPR spills, c4 unchanged.)
 #define YRT_PRIMARY_PERSIST_MIN_ITEMS 0
 #endif
+#ifndef YRT_R5_IDXLANE
+#define YRT_R5_IDXLANE 1
+#endif
 #ifndef YRT_PRIMARY_BLOCK_CHUNK
 #define YRT_PRIMARY_BLOCK_CHUNK 16  // (64: the same)
 #endif
@@ -779,8 +814,8 @@ __global__ __launch_bounds__(YRT_PRIMARY_SP_BLOCK, YRT_PRIMARY_WAVES) void k_pri
         tail_items++;
 #endif
         asm volatile("" ::: "memory");
-        const bool valid =
-            primary_samples<false, true, SE, SPB, LDSN, LIST>(S, A_lds, C_lds, B_lds, T, (int)(it * 64 + lane), wc, lds_rec);
+        const bool valid = primary_samples<false, true, SE, SPB, LDSN, LIST>(S, A_lds, C_lds, B_lds, T,
+                                                                            (int)(it * 64) + (YRT_R5_IDXLANE ? lane_now() : (int)lane), wc, lds_rec);
         valid_n += (unsigned)__popcll(ballot(valid));
     }
 #ifdef YRT_TAIL_STATS
@@ -819,9 +854,7 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
             if (YRT_HIT16) {
                 store_hit16(B, idx, hit, hr);
             } else {
-                surface sf = {};
-                if (hit) sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
-                store_surface(B, idx, hit, sf);
+                store_hit_surface(S, B, idx, hit, hr);
             }
         }
     }
@@ -1189,8 +1222,16 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
             if (e < nc)
                 for (int q = 0; q < 7; q++) v[q] = cand[w][e][q];
         } else {  // the rest of the chain
+            // the union of the later leaves' boxes, a NaN bound sticking: the walk's slab test
+            // ignores a NaN plane, so a leaf with one passes more rays than its finite bounds
+            // say, and the chain box must let all of those through too (fminf / fmaxf alone
+            // would drop the NaN and could narrow the box below that leaf's reach)
             for (int e = 3 * rq + 3; e < nc; e++)
-                for (int q = 0; q < 3; q++) v[q] = fminf(v[q], cand[w][e][q]), v[q + 3] = fmaxf(v[q + 3], cand[w][e][q + 3]);
+                for (int q = 0; q < 3; q++) {
+                    const float lo = cand[w][e][q], hi = cand[w][e][q + 3];
+                    v[q] = (lo != lo || v[q] != v[q]) ? __builtin_nanf("") : fminf(v[q], lo);
+                    v[q + 3] = (hi != hi || v[q + 3] != v[q + 3]) ? __builtin_nanf("") : fmaxf(v[q + 3], hi);
+                }
             v[6] = __uint_as_float((rec0 + rq + 1) * (uint32_t)wide_record_bytes);
         }
         for (int q = 0; q < 7; q++) slot[w][lane][q] = v[q];
@@ -1205,18 +1246,28 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
     if (lane == 0) B.lcount[gl] = nc;
 }
 
-// ---- camera lists: per 8x8-pixel tile of the chunk, the instance-level leaves whose box a
-// camera ray of the tile can pass (packet_first's list mode). The tile's rays start at the
-// camera origin O and run through its pixels' rectangle [i0, i1 + 1] x [j0, j1 + 1] of the
-// image plane (the samples lie strictly inside it, raytrace.cpp:236-239), so they lie in the
-// cone from O through the rectangle's four corners. One wave per tile walks the any-hit
-// tree (its leaves are the reference's, its inner boxes unions of them): lane 16 s + k tests
-// slot s against cone plane k (k < 4), and a box is dropped when it lies outside a plane
-// by more than a margin above the slab test's rounding. The leaves go out in the reference's
-// DFS order (descending first slot), boxes relative to O (the same fp32 (bound - o) as the
-// REL records).
+// ---- camera lists: per 8x8-pixel tile of the chunk, a frontier of the reference's instance
+// tree for packet_first's list mode. The tile's rays start at the camera origin O and run
+// through its pixels' rectangle [i0, i1 + 1] x [j0, j1 + 1] of the image plane (the samples lie
+// strictly inside it, raytrace.cpp:236-239), so they lie in the cone from O through the
+// rectangle's four corners; a box that lies outside a cone plane by more than a margin above
+// the slab test's rounding fails every such ray's exact test (intersect_check_bbox,
+// scene.cpp:371-382) at any tmax.
+//
+// The list is a frontier: disjoint subtrees of the reference's tree (inner nodes or leaves)
+// that together hold every leaf the cone reaches, in the reference's DFS order (child start+1
+// before start, scene.cpp:446-479). One wave per tile grows it from the root, a round per tree
+// level, lane q holding entry q: an inner entry whose children the cone reaches one or none of
+// is replaced by that child (or dropped) -- that never lengthens the list --, and one whose
+// children both stay is replaced by them while the list has room (camera_list_max entries, the
+// earlier entries first), so a small frontier ends as the tile's leaf list and a large one
+// keeps subtrees where the cone splits. Entries are the first 32 bytes of the node's
+// camera-relative spine record (trel: {lo - o, child record offset or first slot}
+// {hi - o, count | leaf}), exactly what the walk reads for that node.
 __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_render_args A, chunk_args C, wf_buffers B) {
-    __shared__ float cand[4][camera_list_max][8];  // per wave: lo.xyz, first, hi.xyz, count
+    constexpr int K = camera_list_max;
+    static_assert(K <= 64, "one list entry per lane");
+    __shared__ float4 fr[4][2][K][2];  // per wave: the frontier, double-buffered
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ntiles = C.npix / (TILE * TILE);
     const int t = blockIdx.x * 4 + w;
@@ -1236,94 +1287,102 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     j0 = uniform(j0), j1 = uniform(j1);
     const float u0 = (float)i0 / (float)A.width, u1 = (float)(i1 + 1) / (float)A.width;
     const float v0 = (float)j0 / (float)A.height, v1 = (float)(j1 + 1) / (float)A.height;
-    const dev_camera& K = A.cam;
+    const dev_camera& Kc = A.cam;
     auto dir = [&](float u, float v) {
-        return vec3f{(u - 0.5f) * K.w * K.xx + (v - 0.5f) * K.h * K.yx - K.focus * K.zx,
-                     (u - 0.5f) * K.w * K.xy + (v - 0.5f) * K.h * K.yy - K.focus * K.zy,
-                     (u - 0.5f) * K.w * K.xz + (v - 0.5f) * K.h * K.yz - K.focus * K.zz};
+        return vec3f{(u - 0.5f) * Kc.w * Kc.xx + (v - 0.5f) * Kc.h * Kc.yx - Kc.focus * Kc.zx,
+                     (u - 0.5f) * Kc.w * Kc.xy + (v - 0.5f) * Kc.h * Kc.yy - Kc.focus * Kc.zy,
+                     (u - 0.5f) * Kc.w * Kc.xz + (v - 0.5f) * Kc.h * Kc.yz - Kc.focus * Kc.zz};
     };
-    const vec3f O = {K.ox, K.oy, K.oz};
-    // the cone plane of this lane (k = lane % 16 < 4): through O and corners k, k + 1
-    const int k = lane & 15;
-    const float cu[4] = {u0, u1, u1, u0}, cv[4] = {v0, v0, v1, v1};
-    vec3f n = {0, 0, 0};
-    if (k < 4) {
-        const vec3f a = dir(cu[k], cv[k]), b = dir(cu[(k + 1) & 3], cv[(k + 1) & 3]);
-        n = cross(a, b);
-        const vec3f c = dir(0.5f * (u0 + u1), 0.5f * (v0 + v1));
-        if (dot(n, c) > 0.0f) n = n * -1.0f;  // the cone on the negative side
-    }
-    const f4* wbase = sgpr_ptr(S.wnodes);
-    // the scene's extent (the root record's children) for the margin
+    const vec3f O = {Kc.ox, Kc.oy, Kc.oz};
+    // the scene's extent (the absolute root box) and the origin, for the margin
     float M = fmaxf(fmaxf(fabsf(O.x), fabsf(O.y)), fabsf(O.z));
     {
-        float4 r[7];
-        ld_wide_record(wbase, (uint32_t)S.wtop_root, r);
-        for (int q = 0; q < 6; q++)
-            M = fmaxf(M, fmaxf(fmaxf(fabsf(r[q].x), fabsf(r[q].y)), fmaxf(fabsf(r[q].z), fabsf(r[q].w))));
+        const float4 rl = ld4(S.tpair), rh = ld4(S.tpair + 1);
+        M = fmaxf(M, fmaxf(fmaxf(fmaxf(fabsf(rl.x), fabsf(rl.y)), fmaxf(fabsf(rl.z), fabsf(rh.x))),
+                           fmaxf(fabsf(rh.y), fabsf(rh.z))));
     }
     const float eps = 1e-3f + 3e-5f * M;
-    const float margin = (fabsf(n.x) + fabsf(n.y) + fabsf(n.z)) * eps;
-    const int s = lane >> 4;
-    int stk = 0, sp = 0, nc = 0;
-    bool overflow = false;
-    uint32_t cur = (uint32_t)S.wtop_root;
-    for (;;) {
-        float4 r[7];
-        ld_wide_record(wbase, cur, r);
-        auto comp = [&](float4 v) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; };
-        const float clx = comp(r[0]) - O.x, cly = comp(r[1]) - O.y, clz = comp(r[2]) - O.z;
-        const float chx = comp(r[3]) - O.x, chy = comp(r[4]) - O.y, chz = comp(r[5]) - O.z;
-        // outside this lane's plane (a NaN bound never separates)
-        const float mn = n.x * (n.x > 0.0f ? clx : chx) + n.y * (n.y > 0.0f ? cly : chy) + n.z * (n.z > 0.0f ? clz : chz);
-        const bool sep = k < 4 && mn > margin;
-        const unsigned long long sm = ballot(sep);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t word = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
-            if (word == wide_leaf || ((sm >> (16 * q)) & 0xffffull)) continue;
-            if (word & wide_leaf) {
-                if (nc == camera_list_max) {
-                    overflow = true;
-                    continue;
-                }
-                if (lane == 0) {
-                    float* e = cand[w][nc];
-                    e[0] = q == 0 ? r[0].x : q == 1 ? r[0].y : q == 2 ? r[0].z : r[0].w;
-                    e[1] = q == 0 ? r[1].x : q == 1 ? r[1].y : q == 2 ? r[1].z : r[1].w;
-                    e[2] = q == 0 ? r[2].x : q == 1 ? r[2].y : q == 2 ? r[2].z : r[2].w;
-                    e[3] = __int_as_float((int)(word & wide_index_mask));
-                    e[4] = q == 0 ? r[3].x : q == 1 ? r[3].y : q == 2 ? r[3].z : r[3].w;
-                    e[5] = q == 0 ? r[4].x : q == 1 ? r[4].y : q == 2 ? r[4].z : r[4].w;
-                    e[6] = q == 0 ? r[5].x : q == 1 ? r[5].y : q == 2 ? r[5].z : r[5].w;
-                    e[7] = __int_as_float((int)((word >> wide_count_shift) & 7u));
-                }
-                nc++;
-            } else {
-                stk = writelane(stk, (int)word, sp);
-                sp++;
+    // cone plane k (through O and corners k, k + 1; the cone on its negative side), computed by
+    // lane k < 4 and read by every lane
+    vec3f n = {0, 0, 0};
+    if (lane < 4) {
+        const float cu[4] = {u0, u1, u1, u0}, cv[4] = {v0, v0, v1, v1};
+        const vec3f a = dir(cu[lane], cv[lane]), b = dir(cu[(lane + 1) & 3], cv[(lane + 1) & 3]);
+        n = cross(a, b);
+        const vec3f c = dir(0.5f * (u0 + u1), 0.5f * (v0 + v1));
+        if (dot(n, c) > 0.0f) n = n * -1.0f;
+    }
+    float pn[4][3], pm[4];
+    for (int k = 0; k < 4; k++) {
+        pn[k][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(n.x), k));
+        pn[k][1] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(n.y), k));
+        pn[k][2] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(n.z), k));
+        pm[k] = (fabsf(pn[k][0]) + fabsf(pn[k][1]) + fabsf(pn[k][2])) * eps;
+    }
+    // a camera-relative box outside some cone plane (a NaN bound never separates)
+    auto outside = [&](float4 lo, float4 hi) {
+        bool o = false;
+        for (int k = 0; k < 4; k++) {
+            const float mn = pn[k][0] * (pn[k][0] > 0.0f ? lo.x : hi.x) + pn[k][1] * (pn[k][1] > 0.0f ? lo.y : hi.y) +
+                             pn[k][2] * (pn[k][2] > 0.0f ? lo.z : hi.z);
+            o = o || mn > pm[k];
+        }
+        return o;
+    };
+    const f4* trel = B.trel;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int nf, cur = 0;
+    {
+        const float4 rl = ld4(trel), rh = ld4(trel + 1);
+        nf = outside(rl, rh) ? 0 : 1;
+        if (lane == 0) fr[w][0][0][0] = rl, fr[w][0][0][1] = rh;
+    }
+    for (int round = 0; round < 64 && nf > 0; round++) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float4 lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0}, alo = lo, ahi = lo, blo = lo, bhi = lo;
+        bool inner = false, ka = false, kb = false;
+        if (lane < nf) {
+            lo = fr[w][cur][lane][0], hi = fr[w][cur][lane][1];
+            inner = !(ubits(hi.w) & leaf_bit);
+            if (inner) {
+                // children start (B) and start + 1 (A): adjacent records, start's at byte offset lo.w
+                const f4* rb = trel + (size_t)((unsigned)ibits(lo.w) / 16u);
+                blo = ld4(rb), bhi = ld4(rb + 1), alo = ld4(rb + spine_record_f4), ahi = ld4(rb + spine_record_f4 + 1);
+                ka = !outside(alo, ahi), kb = !outside(blo, bhi);
             }
         }
-        if (overflow || sp == 0) break;
-        sp--;
-        cur = (uint32_t)__builtin_amdgcn_readlane(stk, sp);
+        const int c = (int)ka + (int)kb;
+        const bool both = inner && c == 2;  // expanding it lengthens the list by one
+        const bool shrink = inner && c < 2;
+        // the list's length with no two-child expansion, then the two-child ones that fit, in order
+        const int size0 = lane < nf ? (shrink ? c : 1) : 0;
+        const unsigned long long b1 = ballot(size0 & 1), b2 = ballot(size0 & 2);
+        const int len0 = __popcll(b1) + 2 * __popcll(b2);
+        const unsigned long long bb = ballot(both);
+        const bool grow = both && __popcll(bb & below) < K - len0;
+        if (!ballot(shrink || grow)) break;
+        const int size = grow ? 2 : size0;
+        const unsigned long long s1 = ballot(size & 1), s2 = ballot(size & 2);
+        const int pos = __popcll(s1 & below) + 2 * __popcll(s2 & below);
+        float4(*dst)[2] = fr[w][cur ^ 1];
+        if (shrink || grow) {
+            int q = pos;
+            if (ka) dst[q][0] = alo, dst[q][1] = ahi, q++;  // the reference visits start+1 first
+            if (kb) dst[q][0] = blo, dst[q][1] = bhi;
+        } else if (lane < nf) {
+            dst[pos][0] = lo, dst[pos][1] = hi;
+        }
+        nf = __popcll(s1) + 2 * __popcll(s2);
+        cur ^= 1;
     }
-    if (overflow) {
-        if (lane == 0) B.ccount[t] = -1;
-        return;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < nf) {
+        f4* out = B.clist + ((size_t)t * camera_list_max + lane) * 2;
+        const float4 lo = fr[w][cur][lane][0], hi = fr[w][cur][lane][1];
+        out[0] = {lo.x, lo.y, lo.z, lo.w};
+        out[1] = {hi.x, hi.y, hi.z, hi.w};
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's candidate stores, before any lane reads them
-    if (lane < nc) {
-        // rank in the reference's DFS order: descending first slot (the slots are distinct)
-        const int first = __float_as_int(cand[w][lane][3]);
-        int rank = 0;
-        for (int q = 0; q < nc; q++) rank += __float_as_int(cand[w][q][3]) > first ? 1 : 0;
-        const float* e = cand[w][lane];
-        f4* out = B.clist + ((size_t)t * camera_list_max + rank) * 2;
-        out[0] = {e[0] - O.x, e[1] - O.y, e[2] - O.z, e[3]};
-        out[1] = {e[4] - O.x, e[5] - O.y, e[6] - O.z, e[7]};
-    }
-    if (lane == 0) B.ccount[t] = nc;
+    if (lane == 0) B.ccount[t] = nf;
 }
 
 // the sums of one chunk's list lengths into B.lstats (a list that fell back to the tree counts
@@ -1894,9 +1953,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     bool list_stats = false;
     ds.last_camera_lists = ds.last_bundles = false;
     if (!ds.list_stats_host) {
-        hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+        // [0, 4): the sums of the last render that built lists (behind list_stats_ev);
+        // [4, 8): the probe's own, so that neither write lands on the other
+        hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 8 * sizeof(unsigned long long), hipHostMallocDefault);
         if (e != hipSuccess) return e;
-        memset(ds.list_stats_host, 0, 4 * sizeof(unsigned long long));
+        memset(ds.list_stats_host, 0, 8 * sizeof(unsigned long long));
     }
     if (!ds.list_stats_ev) {
         hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
@@ -1948,11 +2009,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
             const int nt = C.npix / (TILE * TILE);
             hipLaunchKernelGGL(k_camera_lists, dim3((nt + 3) / 4), dim3(256), 0, stream, ds.view, A, C, Bp);
             hipLaunchKernelGGL(k_list_stats, dim3(64), dim3(256), 0, stream, Bp, nt, 0);
-            e = hipMemcpyAsync(ds.list_stats_host, B.lstats, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+            e = hipMemcpyAsync(ds.list_stats_host + 4, B.lstats, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                stream);
             if (e == hipSuccess) e = hipStreamSynchronize(stream);
             if (e != hipSuccess) return e;
-            const unsigned long long* st = ds.list_stats_host;
+            const unsigned long long* st = ds.list_stats_host + 4;
             const bool on = st[1] == 0 || st[0] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[1];
             ds.camera_lists_on = ds.bundles_on = on;
             ds.lists_probed = true, ds.probe_cam = A.cam, ds.probe_w = A.width, ds.probe_h = A.height, ds.probe_spp = spp;
@@ -1968,8 +2029,8 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         }
         int t = T.begin(phase_lists, stream);
         if (PACKET && pix0 == 0) {
-            // the camera-relative instance-level records of this render (timed with the
-            // primary phase, whose walk reads them)
+            // the camera-relative instance-level records of this render (timed in the lists
+            // phase, YRT_PHASE_LISTS, with the camera lists built from them)
             const int nrec = (int)ds.ntnodes * 2 * spine_len;
             hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
                                ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);

@@ -72,6 +72,7 @@ struct device_scene {
     // behind its kernels; the next render reads them (if they have arrived) and keeps or
     // drops each kind of list. Both ways give the same image.
     unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
+                                                    // of the last render that built lists, then the probe's 4 sums
     hipEvent_t list_stats_ev = nullptr;
     bool list_stats_recorded = false;  // list_stats_ev has been recorded (yrt_scene_tile_lists waits on it)
     bool camera_lists_on = true, bundles_on = true;
