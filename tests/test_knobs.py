@@ -47,6 +47,10 @@ VARIANTS = {
     "YRT_PRIMARY_LDS_RECORDS": ["-DYRT_PRIMARY_LDS_RECORDS=511"],
     "YRT_PRIMARY_WAVES": ["-DYRT_PRIMARY_WAVES=6", "-DYRT_PRIMARY_SP_BLOCK=768"],
     "YRT_FAST_NORMALIZE": ["-DYRT_FAST_NORMALIZE=0"],
+    # round 5: the conservative inner-slot test of the any-hit walk (both forms lost)
+    # and the shadow-ray cull (on by default)
+    "YRT_ANY_CONSERVATIVE": ["-DYRT_ANY_CONSERVATIVE=1"],
+    "YRT_SHADOW_CULL": ["-DYRT_SHADOW_CULL=0"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change
     "YRT_R5_LANE": ["-DYRT_R5_LANE=0", "-DYRT_R5_UORIG=0", "-DYRT_R5_VCONST=0", "-DYRT_R5_IDXLANE=0", "-DYRT_R5_SURF=0"],
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],

@@ -540,6 +540,27 @@ device_scene* device_scene_create(const scene& scn, int device) {
         std::vector<f4> p = pairs(snodes, nb, nn, nb);
         spair.insert(spair.end(), p.begin(), p.end());
     }
+    if (scn.materials.size() > (size_t)mat_index_mask + 1)
+        throw unsupported_error("scene too large (materials > 2^24, unsupported)");
+    // each material's shadow class (yrt_device.h mat_class_shift; wavefront.hip light_term_zero)
+    std::vector<uint32_t> mat_class(scn.materials.size(), 0);
+    for (size_t k = 0; k < scn.materials.size(); k++) {
+        const material& m = scn.materials[k];
+        const float rs = m.rs;
+        const float ns = (rs) ? 2 / std::pow(rs, 4.0f) - 2 : 1e6f;  // raytrace.cpp:144, as in mats below
+        const float lim = 1048576.0f;                                 // 2^20
+        auto small = [&](vec3f c) { return std::fabs(c.x) <= lim && std::fabs(c.y) <= lim && std::fabs(c.z) <= lim; };
+        if (!small(m.kd) || !small(m.ks)) continue;  // (NaN fails too)
+        if (m.ks.x == 0.0f && m.ks.y == 0.0f && m.ks.z == 0.0f) {
+            if (ns >= 0.0f && ns <= 3.402823466e+38f) mat_class[k] = 1;
+        } else {
+            for (int c = mat_class_max; c >= 2; c--)
+                if (ns >= mat_class_ns(c)) {
+                    mat_class[k] = (uint32_t)c;
+                    break;
+                }
+        }
+    }
     for (int ii : scn.bvh.leaf_prims) {
         const instance& ist = scn.instances[ii];
         if (ist.mat < 0 || ist.mat >= (int)scn.materials.size())
@@ -562,7 +583,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
         const uint32_t wr = (uint32_t)wshape_root[ist.shp] * (uint32_t)wide_record_bytes;
         tinst.push_back({f.y.x, f.y.y, f.y.z, as_float((int)(wr | ((uint32_t)shapes[ist.shp].y << 30)))});
         tinst_id.push_back(ii);
-        tinst.push_back({f.z.x, f.z.y, f.z.z, as_float(ist.mat)});
+        tinst.push_back({f.z.x, f.z.y, f.z.z, as_float((int)((uint32_t)ist.mat | mat_class[ist.mat] << mat_class_shift))});
         // .w of the last row: the shape's root node and primitive kind, so a traversal
         // entering the instance needs no dependent fetch of the shape record
         const i4 sh = shapes[ist.shp];

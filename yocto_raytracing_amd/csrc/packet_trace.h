@@ -112,7 +112,7 @@ __device__ __forceinline__ void ld_scalar(const f4* p_, float4 (&out)[N]) {
 // (s_load ... sbase, soffset): one s_lshl instead of a 64-bit address computation
 template <int N>
 __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, float4 (&out)[N]) {
-    static_assert(N == 2 || N == 3 || N == 4 || N == 5, "record count");
+    static_assert(N == 2 || N == 3 || N == 4 || N == 5 || N == 6, "record count");
     const f4* base = sgpr_ptr(base_);
     const unsigned off = (unsigned)__builtin_amdgcn_readfirstlane((int)(index * 16u));
     if constexpr (N == 2) {
@@ -130,7 +130,7 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
         sgpr16 a;
         asm volatile("s_load_dwordx16 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
-    } else {
+    } else if constexpr (N == 5) {
         sgpr16 a;
         sgpr4 b;
         asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx4 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
@@ -138,6 +138,14 @@ __device__ __forceinline__ void ld_scalar_at(const f4* base_, unsigned index, fl
                      : "s"(base), "s"(off));
         out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
         out[4] = rec_of(b, 0);
+    } else {
+        sgpr16 a;
+        sgpr8 b;
+        asm volatile("s_load_dwordx16 %0, %2, %3\n s_load_dwordx8 %1, %2, %3 offset:0x40\n s_waitcnt lgkmcnt(0)"
+                     : "=&s"(a), "=&s"(b)
+                     : "s"(base), "s"(off));
+        out[0] = rec_of(a, 0), out[1] = rec_of(a, 1), out[2] = rec_of(a, 2), out[3] = rec_of(a, 3);
+        out[4] = rec_of(b, 0), out[5] = rec_of(b, 1);
     }
 }
 
@@ -869,22 +877,89 @@ __device__ __forceinline__ void ld_wide_record(const f4* wbase, uint32_t off, fl
     r[4] = rec_of(b, 0), r[5] = rec_of(b, 1), r[6] = rec_of(c, 0);
 }
 
+// ---- a cheaper slab test for the any-hit walk's inner slots ----
+// Any hit does not depend on the order of the walk, only on which leaves are reached, and
+// the reference reaches a leaf exactly when the leaf's own box passes intersect_check_bbox
+// (scene.cpp:371-382): its ancestors' boxes contain it and the test is monotone in the box
+// (the argument of the 4-wide collapse, packet_occluded_wide2). So an inner slot may use
+// any test that passes at least every ray the exact one passes; leaf slots keep the exact
+// test, and the set of leaves reached -- and so the answer -- stays the reference's.
+//
+// The inner test computes each plane distance as one FMA, fma(b, invd, -(o * invd)), instead
+// of (b - o) * invd (a subtraction and a product), and widens the comparison by the error
+// of that form. Per plane, with u = 2^-24, T = (b - o) * invd the real value, e the exact
+// test's value and c the FMA's: |e - T| <= 2.0001u|T|, |c - T| <= u|T| + 1.0001uM, where
+// M = max_a |o_a * invd_a| (the rounding of the per-lane product), so
+// |c - e| <= 3.001u|c| + 1.001uM. Carried through the max/min chains (lo >= tmin > 0 on a
+// passing exact test) and the reference's tmax * 1.00000024, an exact pass implies
+//     lo_c <= hi_c * (1 + 11.1u) + 2.1uM,
+// which the inner test admits with room: lo_c <= fma(hi_c, 1 + 16u, max(16uM, 2^-100))
+// (the floor covers underflow). The inner test is 12 VALU against the exact test's 18.
+// It is taken only when every live lane has a finite invd and M <= 2^100 (a zero direction
+// component or a huge offset makes the wave use the exact test everywhere), and only for
+// single-octant waves (OCT < 8), on nodes whose four slots are all inner (one scalar branch
+// per node). Compile-time switch YRT_ANY_CONSERVATIVE, off: it loses (DESIGN.md §5 round 5:
+// c4 shadow 11.63 -> 12.49 ms per node, 12.91 with a branch per inner slot -- the walk is
+// co-bound by the scalar unit, which the branches load, and the planes cost 6 VGPRs and 6
+// SGPR spills).
+#ifndef YRT_ANY_CONSERVATIVE
+#define YRT_ANY_CONSERVATIVE 0
+#endif
+struct inner_planes {
+    vec3f noci;  // -(o * invd), per lane
+    float marg;  // max(16uM, 2^-100), per lane
+    bool on;     // wave-uniform: the inner slots use the conservative test
+};
+
+__device__ __forceinline__ inner_planes make_inner_planes(vec3f o, vec3f ci, unsigned long long lanes) {
+    inner_planes p;
+    p.noci = {-(o.x * ci.x), -(o.y * ci.y), -(o.z * ci.z)};
+    const float M = fmaxf(fmaxf(fabsf(p.noci.x), fabsf(p.noci.y)), fabsf(p.noci.z));
+    p.marg = fmaxf(M * 0x1p-20f, 0x1p-100f);
+    // (a NaN fails every comparison: that lane turns the test off for the wave)
+    const bool ok = M <= 0x1p100f && fabsf(ci.x) <= 0x1p100f && fabsf(ci.y) <= 0x1p100f && fabsf(ci.z) <= 0x1p100f;
+    p.on = YRT_ANY_CONSERVATIVE && !(ballot(!ok) & lanes);
+    return p;
+}
+
+template <int OCT>
+__device__ __forceinline__ bool box_oct_inner(const inner_planes& P, vec3f invd, float tmin_r, float tmax_r, float lx,
+                                              float ly, float lz, float hx, float hy, float hz) {
+    const float nx = (OCT & 1) ? hx : lx, fx = (OCT & 1) ? lx : hx;
+    const float ny = (OCT & 2) ? hy : ly, fy = (OCT & 2) ? ly : hy;
+    const float nz = (OCT & 4) ? hz : lz, fz = (OCT & 4) ? lz : hz;
+    const float t0x = fmaf(nx, invd.x, P.noci.x), t0y = fmaf(ny, invd.y, P.noci.y), t0z = fmaf(nz, invd.z, P.noci.z);
+    const float t1x = fmaf(fx, invd.x, P.noci.x), t1y = fmaf(fy, invd.y, P.noci.y), t1z = fmaf(fz, invd.z, P.noci.z);
+    const float lo = fmaxf(fmaxf(fmaxf(t0x, t0y), t0z), tmin_r);
+    const float hi = fminf(fminf(fminf(t1x, t1y), t1z), tmax_r);
+    return lo <= fmaf(hi, 1.00000095367431640625f, P.marg);  // 1 + 2^-20
+}
+
 // the slab tests of a wide step on the record r: m[k] = the lanes of `mask` that pass
 // slot k's box (0 for a slot the node does not have: a scalar branch around it), w[k] =
-// slot k's child word
+// slot k's child word. A node of four inner slots takes box_oct_inner when P.on.
 template <int OCT>
 __device__ __forceinline__ void wide_tests(const float4 (&r)[7], vec3f co, vec3f ci, float tmin, float tmax,
-                                           unsigned long long mask, uint32_t (&w)[4], unsigned long long (&m)[4]) {
+                                           const inner_planes& P, unsigned long long mask, uint32_t (&w)[4],
+                                           unsigned long long (&m)[4]) {
     const float lx[4] = {r[0].x, r[0].y, r[0].z, r[0].w}, ly[4] = {r[1].x, r[1].y, r[1].z, r[1].w},
                 lz[4] = {r[2].x, r[2].y, r[2].z, r[2].w}, hx[4] = {r[3].x, r[3].y, r[3].z, r[3].w},
                 hy[4] = {r[4].x, r[4].y, r[4].z, r[4].w}, hz[4] = {r[5].x, r[5].y, r[5].z, r[5].w};
     w[0] = (uint32_t)uniform(ibits(r[6].x)), w[1] = (uint32_t)uniform(ibits(r[6].y));
     w[2] = (uint32_t)uniform(ibits(r[6].z)), w[3] = (uint32_t)uniform(ibits(r[6].w));
+    if (YRT_ANY_CONSERVATIVE && OCT < 8 && P.on && !((w[0] | w[1] | w[2] | w[3]) & wide_leaf)) {
+        // a node of four inner slots: all four take the inner test, one branch per node
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            m[k] = ballot(box_oct_inner<OCT < 8 ? OCT : 0>(P, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) &
+                   mask;
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        if (k < 2 || w[k] != wide_leaf)  // every wide node has >= 2 slots but a leaf root's 1
+        if (k < 2 || w[k] != wide_leaf) {  // every wide node has >= 2 slots but a leaf root's 1
             m[k] = ballot(box_oct<OCT>(co, ci, tmin, tmax, lx[k], ly[k], lz[k], hx[k], hy[k], hz[k])) & mask;
-        else
+        } else
             m[k] = 0;
     }
 }
@@ -896,11 +971,12 @@ __device__ __forceinline__ void wide_tests(const float4 (&r)[7], vec3f co, vec3f
 // they pop in slot order. Returns true to continue the descent from `cur`.
 template <int OCT>
 __device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f ci, float tmin, float tmax,
+                                          const inner_planes& P,
                                           uint32_t& cur, unsigned long long& mask, int& sp, int& stk_word,
                                           int& stk_mlo, int& stk_mhi, int floor, unsigned long long done) {
     uint32_t w[4];
     unsigned long long m[4];
-    wide_tests<OCT>(r, co, ci, tmin, tmax, mask, w, m);
+    wide_tests<OCT>(r, co, ci, tmin, tmax, P, mask, w, m);
     unsigned long long cm = 0;
     uint32_t cw = 0;
     // the select chain as written for the scalar unit. Chain A tests the slots from the
@@ -1030,6 +1106,7 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f 
 // packet_occluded_wide2)
 template <int OCT, int LDSN>
 __device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, vec3f co, vec3f ci,
+                                             const inner_planes& P,
                                              float tmin, float tmax, uint32_t& cur, unsigned long long& mask,
                                              int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
                                              unsigned long long done, unsigned& nsteps) {
@@ -1044,11 +1121,11 @@ __device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, 
             const float4* p = lds + (cur >> 4);
 #pragma unroll
             for (int k = 0; k < 7; k++) r[k] = p[k];
-            more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
+            more = wide_step<OCT>(r, co, ci, tmin, tmax, P, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         } else {
             float4 r[7];
             ld_wide_record(wbase, cur, r);
-            more = wide_step<OCT>(r, co, ci, tmin, tmax, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
+            more = wide_step<OCT>(r, co, ci, tmin, tmax, P, cur, mask, sp, stk_word, stk_mlo, stk_mhi, floor, done);
         }
         if (!more) return;
     }
@@ -1094,6 +1171,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     vec3f icd, ici;
     enter_direction(frame3f{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}, wd, live, icd, ici);
     const int ioct = wave_octant(ici, live);
+    // the inner slots' conservative planes of the current level (recomputed with co / ci)
+    inner_planes ip = make_inner_planes(wo, wi, live);
     unsigned nsteps0 = 0, nsteps1 = 0;
 #ifdef YRT_WIDE_STATS
     unsigned ws[16] = {1, 0, 0, 0, 0, 0, 0, 0};
@@ -1105,7 +1184,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             DBG_CHECK(((level == 0 && tbase != S.wnodes) || cur < (uint32_t)S.nwnodes * wide_record_bytes) && sp >= 0 &&
                           sp < 61, 4, (int)cur, sp, level,
                       base, 0);
-#define YRT_WD(o) wide_descend<o, LDSN>(level ? S.wnodes : tbase, lds, co, ci, tmin, tmax, cur, mask, sp, stk_word, \
+#define YRT_WD(o) wide_descend<o, LDSN>(level ? S.wnodes : tbase, lds, co, ci, ip, tmin, tmax, cur, mask, sp, stk_word, \
                                          stk_mlo, stk_mhi, wfloor, done, level ? nsteps1 : nsteps0)
             switch (oct) {
                 case 0: YRT_WD(0); break;
@@ -1201,6 +1280,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     }
                     WSTAT(3, 1u);
                     oct = ident ? ioct : wave_octant(ci, live & ~done);
+                    ip = make_inner_planes(co, ci, mask);
                     if (mask) break;
                     continue;
                 }
@@ -1209,6 +1289,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                 cd = wd;
                 ci = wi;
                 oct = woct;
+                ip = make_inner_planes(wo, wi, live & ~done);
             }
             if (sp == 0) {
                 finished = true;

@@ -422,6 +422,7 @@ struct surface {
     vec3f p, n;
     vec2f uv;
     int mat, kind;
+    int mcls;  // the material's shadow class (yrt_device.h mat_class_shift)
 };
 
 #ifndef YRT_FAST_NORMALIZE
@@ -458,7 +459,8 @@ __device__ __forceinline__ surface eval_surface(const dev_scene_view& S, int slo
     int4 sh = ld4(S.shapes + (ibits(fx.w) & (int)inst_shape_mask));
     int4 e = ld4(S.elems + sh.z + ei);
     surface sf;
-    sf.mat = ibits(fz.w);
+    sf.mat = (int)((uint32_t)ibits(fz.w) & mat_index_mask);
+    sf.mcls = (int)((uint32_t)ibits(fz.w) >> mat_class_shift);
     sf.kind = sh.y;
     vec3f lp, ln;
     vec2f luv;

@@ -12,7 +12,8 @@
 //               mirror ray, compacted into the next level with one ballot + one
 //               atomic per wave
 //   (levels 1..max_depth-1: k_bounce (closest hit of the compacted rays), k_shadow,
-//    k_shade; then k_fold back to front: R_k = (D_k + R_{k+1}*kr_k) + la_k)
+//    k_shade; a sample whose value is final folds it up its chain of parents at once:
+//    R_k = (D_k + R_{k+1}*kr_k) + la_k)
 //   k_accumulate  the ordered per-pixel sum of raytrace.cpp:232-249
 //
 // Why: every traversal kernel carries only its ray and stack (few VGPRs, high
@@ -276,6 +277,11 @@ __device__ __forceinline__ void store_hit16(const wf_buffers& B, int idx, bool h
 // conditional aggregate copy kept the first 28 bytes of sf in a private array, which the
 // backend promoted to 28 KB of LDS per 1024-thread block; its 64-bit address then took
 // VGPRs the closest-hit walk spilled to scratch.)
+// the surface record's info word: shadow class << 26 | material << 2 | kind (material < 2^24,
+// so a hit's info is >= 0; -1 miss, -2 not a sample)
+__device__ __forceinline__ int surf_info(const surface& sf) { return sf.mcls << 26 | sf.mat << 2 | sf.kind; }
+__device__ __forceinline__ int info_mat(int info) { return (info >> 2) & (int)mat_index_mask; }
+
 __device__ __forceinline__ vec3f store_hit_surface(const dev_scene_view& S, const wf_buffers& B, int idx, bool hit,
                                                    const hit_record& hr) {
     if (!hit) {
@@ -283,7 +289,7 @@ __device__ __forceinline__ vec3f store_hit_surface(const dev_scene_view& S, cons
         return {0, 0, 0};
     }
     const surface sf = eval_surface(S, hr.slot, hr.ei, hr.ew);
-    gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind));
+    gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(surf_info(sf)));
     gstore(B.surf1, idx, sf.n.x, sf.n.y, sf.n.z, sf.uv.x);
     // uv is read only by texture lookups: a scene without textures never needs it
     if (!YRT_SKIP_UNUSED_V || B.need_v) gstore(B.surfv, idx, sf.uv.y);
@@ -364,6 +370,50 @@ __device__ __forceinline__ vec3f div3(vec3f ke, float rr) {
         return {div_nr(ke.x, rr, y), div_nr(ke.y, rr, y), div_nr(ke.z, rr, y)};
     }
     return ke / rr;
+}
+
+#ifndef YRT_SHADOW_CULL
+#define YRT_SHADOW_CULL 1
+#endif
+// ---- shadow rays whose light term is exactly zero are not traced ----
+// shade() (raytrace.cpp:133-183) adds a light's term c += ld + ls only when intersect_any
+// finds no occluder; skipping it and adding it are the same when the term is +-0 in every
+// component (c starts at +0 and a sum never turns into -0 under round-to-nearest, so c + +-0
+// is c bit for bit). From the hit's material class (yrt_device.h mat_class_shift, set at
+// upload) and the geometry alone, the term is +-0 when max(0, n.l) is +-0 and ker = ke / r^2
+// is below 2^100 in every component -- then ld = (kd0 * tkd) * ker * max(0, n.l) is a finite
+// product (|kd0| <= 2^20, the texture factor in [0, 1]) times +-0 -- and ls is +-0:
+//   class 1 (Ks == 0, ns in [0, FLT_MAX]): ks * ker is +-0, and with x = max(0, n.h) in
+//     [0, 1] spec_pow takes its shortcut (factor 1), so ls = +-0;
+//   class c >= 2 (ns >= mat_class_ns(c) > 0, |Ks| <= 2^20): powf_cr(x, ns) is exactly 0 when
+//     x == 0, or when x in [2^-126, 1) and ns * log2(x) < -151 by v_log_f32 -- which
+//     mat_class_ns(c) * log2(x) < -151 implies (log2(x) < 0, and rounding is monotone) --, so
+//     ls = finite * 0; where spec_pow takes its shortcut instead, ls = +-0 * 1.
+// n, l, r, v, h and ker are computed with the functions k_shade uses (normalize_len, div3),
+// so the test sees k_shade's values.
+// Lines (their sin-based lighting) are always traced. A culled ray is recorded as occluded:
+// k_shade skips the light, which leaves c as adding +-0 would. The ray counters keep the
+// reference's counts (a culled ray is counted); the instrumented COUNT pass traces every ray.
+// n is the surface record's second row, loaded beside the first: no dependent load.
+// Called in uniform control flow; a wave in which no lane can pass the cheap first tests
+// (class, kind, max(0, n.l) == 0) skips the rest.
+__device__ __forceinline__ bool light_term_zero(int info, vec3f nrm, vec3f p, vec3f ro, vec3f l, float r, vec3f ke) {
+    const int cls = (info >> 26) & 15;
+    const float sd = smax(0.0f, dot(nrm, l));
+    const bool first = info >= 0 && cls != 0 && (info & 3) != kind_lines && sd == 0.0f;
+    if (!ballot(first)) return false;
+    vec3f v, h, ker;
+    float vlen, hlen;
+    normalize_len(ro - p, v, vlen);
+    normalize_len(v + l, h, hlen);
+    ker = div3(ke, r * r);
+    const float x = smax(0.0f, dot(nrm, h));
+    const bool ker_ok = fabsf(ker.x) < 0x1p100f && fabsf(ker.y) < 0x1p100f && fabsf(ker.z) < 0x1p100f;
+    const bool ls_zero =
+        cls == 1 ? x >= 0.0f && x <= 1.0f
+                 : x == 0.0f || (x >= 0x1p-126f && x < 1.0f &&
+                                 (float)(16 << ((cls - 2) & 15)) * __builtin_amdgcn_logf(x) < -151.0f);
+    return first && ker_ok && ls_zero;
 }
 
 // camera_ray (trace_common.h, raytrace.cpp:6-37 with the uv of :235-238) with its four
@@ -580,7 +630,7 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
             if (!hit)
                 gstore(B.surf0, idx, 0, 0, 0, __int_as_float(-1));
             else {
-                gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(sf.mat * 4 + sf.kind));
+                gstore(B.surf0, idx, sf.p.x, sf.p.y, sf.p.z, __int_as_float(surf_info(sf)));
                 gstore(B.surf1, idx, sf.n.x, sf.n.y, sf.n.z, sf.uv.x);
                 if (!YRT_SKIP_UNUSED_V || B.need_v) gstore(B.surfv, idx, sf.uv.y);
             }
@@ -869,7 +919,8 @@ __global__ __launch_bounds__(WF_BLOCK, YRT_TRACE_WAVES) void k_bounce(dev_scene_
 template <bool COUNT, bool PACKET, typename SE, bool WIDE>
 __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_shadow(dev_scene_view S, int level,
                                                                      int nsamp_level0, wf_buffers B,
-                                                                     unsigned long long* counters) {
+                                                                     unsigned long long* counters, float4 cam4) {
+    const vec3f cam_o = xyz(cam4);  // the camera rays' origin (level 0's view point)
     constexpr int BS = shadow_block<PACKET>();
     __shared__ traversal_lds<PACKET, SE> lds;
     auto T = make_tracer<true, COUNT, PACKET, SE>(lds);
@@ -883,7 +934,7 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     const int bx = level ? (int)blockIdx.x : (int)(lin / gridDim.y);
     const f4* lr = S.lights + 6 * li;
     const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
-    const vec3f lp0 = xyz(ld4(lr + 4));
+    const vec3f lp0 = xyz(ld4(lr + 4)), ke = xyz(ld4(lr + 5));
     work_counts wc;
     unsigned long long rays = 0;
     const int stride = gridDim.x * BS;
@@ -894,18 +945,32 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
         const int j = round * stride + bx * BS + threadIdx.x;
         const int idx = g * B.seg + j;
         bool valid = false;
+        int info = -1;
+        float r = 1.0f;
+        float4 s1 = {0, 0, 0, 0}, ro4 = make_float4(cam_o.x, cam_o.y, cam_o.z, 0.0f);
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
+        constexpr bool CULL = YRT_SHADOW_CULL && !COUNT && !YRT_HIT16;
         if (j < n) {
             float4 s0 = ld4s(B.surf0 + idx);
-            if (sample_state(s0) >= 0) {
+            if (CULL) {  // n and the view point, for light_term_zero
+                s1 = ld4s(B.surf1 + idx);
+                if (level) ro4 = ld4(B.ray_o(level) + idx);
+            }
+            info = sample_state(s0);
+            if (info >= 0) {
                 const vec3f p = YRT_HIT16 ? hit16_surface(S, s0).p : xyz(s0);
                 vec3f tp = transform_point(lf, lp0 - p);
                 vec3f l;
-                float r;
                 normalize_len(tp, l, r);
                 sr = {p, l, 0.01f, r - 0.01f};
                 valid = true;
                 rays++;
+            }
+        }
+        if (CULL) {  // (uniform control flow; a lane that is not a hit has info < 0)
+            if (light_term_zero(info, xyz(s1), sr.o, xyz(ro4), sr.d, r, ke)) {
+                stb(B.occl + (size_t)li * B.capacity + idx, 1);
+                valid = false;
             }
         }
         hit_record hr;
@@ -1441,7 +1506,9 @@ __global__ __launch_bounds__(256) void k_list_stats(wf_buffers B, int ntiles, in
 template <int LDSN>
 __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(dev_scene_view S, int nsamp,
                                                                                 int nx, wf_buffers B,
-                                                                                unsigned long long* counters) {
+                                                                                unsigned long long* counters,
+                                                                                float4 cam4) {
+    const vec3f cam_o = xyz(cam4);  // the camera rays' origin: the view point of level 0's shading
     constexpr int WPB = SP_BLOCK / 64;  // waves per block
     constexpr unsigned C = YRT_SHADOW_LIGHT_MINOR;
     __shared__ float4 lds_nodes[LDSN > 0 ? LDSN * 8 : 1];
@@ -1475,26 +1542,37 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         const int li = (int)(it % (unsigned)nl);
         const int bx = (int)(it / (unsigned)nl);
         // the light's frame and position: one wave-uniform record, through the scalar cache
-        float4 lrec[5];
-        ld_records_at<5>(S.lights, (unsigned)(6 * li), lrec);
+        float4 lrec[6];
+        ld_records_at<6>(S.lights, (unsigned)(6 * li), lrec);
         const frame3f lf = {xyz(lrec[0]), xyz(lrec[1]), xyz(lrec[2]), xyz(lrec[3])};
         const vec3f lp0 = xyz(lrec[4]);
         const int idx = bx * 64 + (int)lane;
         bool valid = false;
+        int info = -1;
+        float r = 1.0f;
+        float4 s1 = {0, 0, 0, 0};
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
         if (idx < nsamp) {
             float4 s0 = ld4s(B.surf0 + idx);
-            if (sample_state(s0) >= 0) {
+            if (YRT_SHADOW_CULL && !YRT_HIT16) s1 = ld4s(B.surf1 + idx);  // n, for light_term_zero
+            info = sample_state(s0);
+            if (info >= 0) {
                 const vec3f p = YRT_HIT16 ? hit16_surface(S, s0).p : xyz(s0);
                 vec3f tp = transform_point(lf, lp0 - p);
                 vec3f l;
-                float r;
                 normalize_len(tp, l, r);
                 sr = {p, l, 0.01f, r - 0.01f};
                 valid = true;
             }
         }
         rays += (unsigned)__popcll(ballot(valid));
+        // a wave whose every ray has a zero light term skips the walk (per-lane culling inside
+        // this loop trips the compiler: "illegal VGPR to SGPR copy"; the 64 rays of a wave are
+        // one pixel's samples at c4, so they agree). light_term_zero runs in uniform control
+        // flow: its loads and ballots on every lane.
+        const bool all_culled =
+            YRT_SHADOW_CULL && !YRT_HIT16 &&
+            !ballot(valid && !light_term_zero(info, xyz(s1), sr.o, cam_o, sr.d, r, xyz(lrec[5])));
         bool occ;
         int lc = -1;  // the bundle's list: its leaf count, -1 = walk the tree
         if (YRT_SHADOW_BUNDLES && LDSN == 0 && B.bundles) {
@@ -1507,8 +1585,9 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
             tbase = B.lists;
             troot = (uint32_t)(((bx / bundle_g) * nl + li) * bundle_recs * wide_record_bytes);
         }
-        // lc == 0: no leaf can be passed by these rays, none is occluded
-        occ = lc == 0 ? false : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot);
+        // lc == 0: no leaf can be passed by these rays, none is occluded; all_culled: recorded
+        // as occluded, k_shade skips the light
+        occ = all_culled ? true : lc == 0 ? false : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot);
         if (valid) stb(B.occl + (size_t)li * B.capacity + idx, occ ? 1 : 0);
     }
 #ifdef YRT_TAIL_STATS
@@ -1611,7 +1690,7 @@ __global__ __launch_bounds__(SB, FUSE ? YRT_SHADE_WAVES : YRT_SHADE_LEVEL_WAVES)
                 } else {
                     const float4 s1 = ld4s(B.surf1 + idx);
                     p = xyz(s0), nrm = xyz(s1), uv = {s1.w, (!YRT_SKIP_UNUSED_V || B.need_v) ? lds1(B.surfv + idx) : 0.0f};
-                    mat = info >> 2, kind = info & 3;
+                    mat = info_mat(info), kind = info & 3;
                 }
                 const vec3f ro = xyz(ro4);
                 float4 m0, m1, m2, m3;
@@ -1672,7 +1751,8 @@ __global__ __launch_bounds__(SB, FUSE ? YRT_SHADE_WAVES : YRT_SHADE_LEVEL_WAVES)
                 }
                 if (!reflective) {
                     R = c + la;
-                } else if (level + 1 >= max_depth || level + 1 >= B.nlevels) {
+                } else if (FUSE || level + 1 >= max_depth || level + 1 >= B.nlevels) {
+                    // (FUSE runs one-level renders: B.nlevels == 1, no mirror ray is spawned)
                     // depth cap: the reflected contribution counts as a miss (col = 0)
                     truncated++;
                     vec3f t = {0.0f * kr.x, 0.0f * kr.y, 0.0f * kr.z};
@@ -1973,6 +2053,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         if (e != hipSuccess) return e;
     }
     phase_timer& T = ds.timer;
+    const float4 cam4 = make_float4(A.cam.ox, A.cam.oy, A.cam.oz, 0.0f);
     const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
     // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE;
     // one-wave fused blocks lose: +9 %)
@@ -2110,16 +2191,16 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                     constexpr int L = YRT_SHADOW_LDS_RECORDS;
                     if (L > 0 && ds.view.nwtop >= L)
                         hipLaunchKernelGGL((k_shadow_persist<L>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
-                                           nsamp, tgrid, B, counters);
+                                           nsamp, tgrid, B, counters, cam4);
                     else
                         hipLaunchKernelGGL((k_shadow_persist<0>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
-                                           nsamp, tgrid, B, counters);
+                                           nsamp, tgrid, B, counters, cam4);
                 } else if (!COUNT && PACKET && ds.wide_ok)
                     hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, true>), sg, dim3(TB), 0,
-                                       stream, ds.view, level, nsamp, B, counters);
+                                       stream, ds.view, level, nsamp, B, counters, cam4);
                 else
                     hipLaunchKernelGGL((k_shadow<COUNT, PACKET, SE, false>), sg, dim3(TB), 0,
-                                       stream, ds.view, level, nsamp, B, counters);
+                                       stream, ds.view, level, nsamp, B, counters, cam4);
                 T.end(t, stream);
             }
             t = T.begin(phase_shade, stream);

@@ -49,6 +49,15 @@ constexpr uint32_t leaf_bit = 0x80000000u;
 // tinst row 0 .w: set when the instance frame's rotation rows are bitwise the identity's
 constexpr uint32_t inst_identity_bit = 0x40000000u;
 constexpr uint32_t inst_shape_mask = 0x3fffffffu;
+// tinst row 2 .w: the material index | its shadow class << mat_class_shift. The class says
+// when a light's term for a hit on the material is +-0 from the geometry alone, so that its
+// shadow ray need not be traced (wavefront.hip light_term_zero): 0 never; 1 no specular
+// (Ks == 0, ns in [0, FLT_MAX], |Kd| <= 2^20); c >= 2 specular with ns >= mat_class_ns(c)
+// (|Kd|, |Ks| <= 2^20). Materials are limited to 2^24.
+constexpr int mat_class_shift = 24;
+constexpr uint32_t mat_index_mask = 0x00ffffffu;
+constexpr int mat_class_max = 15;
+constexpr float mat_class_ns(int c) { return (float)(16 << (c - 2)); }  // c in [2, 15]: 16 .. 131072
 
 // winst (the any-hit walk's instance records) packs what that walk reads into five rows --
 // {frame.x, tinst row 0 .w} {frame.y, wide root | kind} {frame.z, box lo.x}
