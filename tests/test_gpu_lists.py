@@ -1,6 +1,6 @@
 """The per-tile candidate lists of the render path: camera lists
 (k_camera_lists, packet_first's list mode) and shadow bundles (k_bundle_lists). Lists are
-an acceleration only: with them forced on, forced off, or chosen by the per-view probe the
+an acceleration only: with them forced on, forced off, or in the default (auto) mode the
 image is the same, and it equals the oracle (the reference's raytrace(),
 src/raytrace.cpp:213-254) -- on ragged frames whose 8x8-pixel tiles are cut by the frame's
 edge, sample counts whose 64-sample items straddle pixels, windows, lists that overflow
@@ -85,15 +85,17 @@ def test_lists_on_in_a_window(yrt):
     check_oracle(on, ref, "instance10000 window lists on")
 
 
-def test_lists_auto_probe(yrt):
-    """the per-view probe (auto): instance10000's lists average ~4 leaves at c4 and are used,
-    instance100k's ~18 and are not; the image is the forced-off image either way"""
-    for name, used in (("instance10000", True), ("instance100k", False)):
+def test_lists_auto(yrt):
+    """auto builds both kinds of list on the instance scenes at c4 settings -- the camera lists
+    are frontiers of at most camera_list_max entries, so none falls back to the tree -- and
+    the image is the forced-off image (instance100k: 17.8 leaves per tile as leaf lists, which
+    round 4's probe turned off; as frontiers they take its closest hit 26.6 -> 25.3 ms)"""
+    for name in ("instance10000", "instance100k"):
         ds = host(yrt, name).upload(0)
         auto, _, la = render(yrt, ds, "auto", 1080, 8)
-        assert la["camera"] == used and la["bundles"] == used, (name, la)
-        if used:
-            assert la["camera_entries"] <= 6 * la["camera_lists"]
+        assert la["camera"] and la["bundles"], (name, la)
+        assert 0 < la["camera_entries"] <= 32 * la["camera_lists"], (name, la)
+        print(name, la)
         off, _, _ = render(yrt, ds, "off", 1080, 8)
         np.testing.assert_array_equal(auto.view(np.uint32), off.view(np.uint32))
         del ds
@@ -172,7 +174,7 @@ def test_tile_lists_argument_errors(yrt):
 def test_lists_follow_the_view(yrt):
     """one scene handle rendered from each of instance10000's five cameras in turn and back
     to the first (`camera` selects scn->cameras[k]; the reference always takes the first,
-    raytrace.cpp:225): each new view is probed again, and every frame -- probed, forced on
+    raytrace.cpp:225): each new view gets its own lists, and every frame -- auto, forced on
     or off -- equals the oracle's render from that camera"""
     name, res, spp = "instance10000", 180, 4
     ds = host(yrt, name).upload(0)

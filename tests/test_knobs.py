@@ -40,7 +40,7 @@ VARIANTS = {
     "YRT_HIT16": ["-DYRT_HIT16=1"],
     "YRT_SHADOW_BUNDLES": ["-DYRT_SHADOW_BUNDLES=0"],
     "YRT_CAMERA_LISTS": ["-DYRT_CAMERA_LISTS=0"],
-    "YRT_CAMERA_LIST_MAX": ["-DYRT_CAMERA_LIST_MAX=12", "-DYRT_LIST_MAX_MEAN=4"],
+    "YRT_CAMERA_LIST_MAX": ["-DYRT_CAMERA_LIST_MAX=12"],
     "YRT_BUNDLE_ITEMS": ["-DYRT_BUNDLE_ITEMS=16", "-DYRT_BUNDLE_MIN_TOP=0"],
     "YRT_SKIP_UNUSED_V": ["-DYRT_SKIP_UNUSED_V=0"],
     "YRT_SHADE_LEVEL_WAVES": ["-DYRT_SHADE_LEVEL_WAVES=7"],
@@ -60,7 +60,7 @@ VARIANTS = {
                           "-DYRT_PRIMARY_BLOCK_CHUNK=64"],
 }
 # knobs covered by another entry's defines
-COVERED = {"YRT_R5_UORIG", "YRT_R5_VCONST", "YRT_R5_IDXLANE", "YRT_R5_SURF", "YRT_LIST_MAX_MEAN", "YRT_BUNDLE_MIN_TOP", "YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
+COVERED = {"YRT_R5_UORIG", "YRT_R5_VCONST", "YRT_R5_IDXLANE", "YRT_R5_SURF", "YRT_BUNDLE_MIN_TOP", "YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
            "YRT_SHADOW_PERSIST_MIN_ITEMS", "YRT_PRIMARY_PERSIST_MIN_ITEMS", "YRT_PRIMARY_BLOCK_CHUNK"}
 
 

@@ -491,13 +491,6 @@ constexpr int bundle_max_lights = 8;  // more lights: no bundles (the lists' mem
 #define YRT_CAMERA_LIST_MAX 32  // leaves per tile list (more: the tile's rays walk the tree)
 #endif
 constexpr int camera_list_max = YRT_CAMERA_LIST_MAX;
-#ifndef YRT_LIST_MAX_MEAN
-// a kind of list stays on while its lists average at most this many leaves (a list that fell
-// back to the tree counts as its capacity + 1): longer lists cost more than the tree walk they
-// replace (A/B: instance10000 3.8 / 4.3 leaves per camera / bundle list, -6 % per frame;
-// instance100k 17.8 / 9.2, +2 to +4 %)
-#define YRT_LIST_MAX_MEAN 6
-#endif
 
 // wave-wide min / max with DPP row rotations and row broadcasts (VALU only, no LDS round
 // trips): every row of 16 lanes folds itself, rows 1 and 3 take rows 0 and 2 (row_bcast:15),
@@ -2016,28 +2009,13 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     B.trel = ds.trel;
     B.seg = seg;
     B.need_v = ds.view.ntextures > 0;
-    // a new view is probed (below); otherwise the list sums of an earlier render, if they have
-    // arrived, keep or drop each kind of list
-    if (ds.lists_probed && (memcmp(&ds.probe_cam, &A.cam, sizeof(dev_camera)) != 0 || ds.probe_w != A.width ||
-                            ds.probe_h != A.height || ds.probe_spp != spp))
-        ds.lists_probed = false;
-    if (ds.lists_probed && ds.list_stats_ev && hipEventQuery(ds.list_stats_ev) == hipSuccess) {
-        const unsigned long long* st = ds.list_stats_host;
-        static const bool debug = getenv("YRT_LIST_DEBUG") != nullptr;  // diagnostic: the lists' mean lengths
-        if (debug)
-            fprintf(stderr, "yrt lists: camera %llu entries / %llu tiles, bundles %llu entries / %llu lists\n", st[0],
-                    st[1], st[2], st[3]);
-        if (st[1]) ds.camera_lists_on = st[0] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[1];
-        if (st[3]) ds.bundles_on = st[2] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[3];
-    }
     bool list_stats = false;
     ds.last_camera_lists = ds.last_bundles = false;
     if (!ds.list_stats_host) {
-        // [0, 4): the sums of the last render that built lists (behind list_stats_ev);
-        // [4, 8): the probe's own, so that neither write lands on the other
-        hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 8 * sizeof(unsigned long long), hipHostMallocDefault);
+        // the sums of the last render that built lists (behind list_stats_ev)
+        hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
         if (e != hipSuccess) return e;
-        memset(ds.list_stats_host, 0, 8 * sizeof(unsigned long long));
+        memset(ds.list_stats_host, 0, 4 * sizeof(unsigned long long));
     }
     if (!ds.list_stats_ev) {
         hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
@@ -2079,29 +2057,9 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         // the camera rays walk their tiles' leaf lists (k_camera_lists)
         const bool cam_lists_possible = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
                                         ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
-        if (cam_lists_possible && ds.lists_mode == 0 && !ds.lists_probed && pix0 == 0) {
-            // probe this view: sum the first chunk's camera lists and wait for the sum; both kinds
-            // of list follow it (their lengths go together: instance10000 3.8 / 4.3 leaves,
-            // instance100k 17.8 / 9.2), later renders refine each from its own sums
-            wf_buffers Bp = B;
-            Bp.cam_lists = 1, Bp.bundles = 0;
-            hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);
-            if (e != hipSuccess) return e;
-            const int nt = C.npix / (TILE * TILE);
-            hipLaunchKernelGGL(k_camera_lists, dim3((nt + 3) / 4), dim3(256), 0, stream, ds.view, A, C, Bp);
-            hipLaunchKernelGGL(k_list_stats, dim3(64), dim3(256), 0, stream, Bp, nt, 0);
-            e = hipMemcpyAsync(ds.list_stats_host + 4, B.lstats, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                               stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(stream);
-            if (e != hipSuccess) return e;
-            const unsigned long long* st = ds.list_stats_host + 4;
-            const bool on = st[1] == 0 || st[0] <= (unsigned long long)YRT_LIST_MAX_MEAN * st[1];
-            ds.camera_lists_on = ds.bundles_on = on;
-            ds.lists_probed = true, ds.probe_cam = A.cam, ds.probe_w = A.width, ds.probe_h = A.height, ds.probe_spp = spp;
-        }
-        // (YRT_LISTS_ON / _OFF: the caller's choice, yrt_scene_set_tile_lists)
-        B.cam_lists = cam_lists_possible && (ds.lists_mode == 1 || (ds.lists_mode == 0 && ds.camera_lists_on));
-        B.bundles = bundles_possible && (ds.lists_mode == 1 || (ds.lists_mode == 0 && ds.bundles_on));
+        // (YRT_LISTS_AUTO / _ON: whenever the scene allows; _OFF: never -- yrt_scene_set_tile_lists)
+        B.cam_lists = cam_lists_possible && ds.lists_mode != 2;
+        B.bundles = bundles_possible && ds.lists_mode != 2;
         ds.last_camera_lists |= B.cam_lists != 0, ds.last_bundles |= B.bundles != 0;
         if ((B.cam_lists || B.bundles) && !list_stats) {
             list_stats = true;

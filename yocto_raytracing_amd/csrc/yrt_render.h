@@ -67,22 +67,16 @@ struct device_scene {
     // mirror levels: the next level's ray count, copied back behind the level's kernels
     int* level_count_host = nullptr;  // pinned
     hipEvent_t level_count_ev = nullptr;
-    // the candidate lists (wavefront.hip k_camera_lists / k_bundle_lists) pay only when they
-    // are short: each render sums its lists' lengths on the device and copies the sums back
-    // behind its kernels; the next render reads them (if they have arrived) and keeps or
-    // drops each kind of list. Both ways give the same image.
+    // the candidate lists (wavefront.hip k_camera_lists / k_bundle_lists): each render that
+    // builds them sums their lengths on the device and copies the sums back behind its kernels
+    // (yrt_scene_tile_lists reads them). Lists on or off give the same image.
     unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
-                                                    // of the last render that built lists, then the probe's 4 sums
     hipEvent_t list_stats_ev = nullptr;
     bool list_stats_recorded = false;  // list_stats_ev has been recorded (yrt_scene_tile_lists waits on it)
-    bool camera_lists_on = true, bundles_on = true;
-    int lists_mode = 0;  // YRT_LISTS_AUTO (the above) / YRT_LISTS_ON / YRT_LISTS_OFF (yrt_scene_set_tile_lists)
+    // YRT_LISTS_AUTO / YRT_LISTS_ON: lists whenever the scene allows (ON also puts level 0's
+    // shadow rays on the persistent grid at any frame size); YRT_LISTS_OFF: never
+    int lists_mode = 0;
     bool last_camera_lists = false, last_bundles = false;  // what the last render used
-    // the view the lists were last probed for (a first render, or a new camera or image size,
-    // probes: its first chunk's camera lists are summed before its walks run)
-    bool lists_probed = false;
-    dev_camera probe_cam = {};
-    int probe_w = 0, probe_h = 0, probe_spp = 0;
     phase_timer timer;
 };
 
