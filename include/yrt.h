@@ -82,7 +82,9 @@ typedef struct yrt_stats {
     unsigned long long prim_tests;
     unsigned long long shaded_hits;
     unsigned long long texture_lookups;
-    unsigned long long shadow_rays;     /* the shadow-ray phase alone (intersect_any calls) */
+    unsigned long long shadow_rays;     /* the shadow-ray phase alone (intersect_any calls; the
+                                         * reference's count: a shadow ray whose light term is
+                                         * exactly zero is counted but not traced) */
     unsigned long long shadow_box_tests;        /* count_work only */
     unsigned long long shadow_instance_entries; /* count_work only */
     unsigned long long shadow_prim_tests;       /* count_work only */
