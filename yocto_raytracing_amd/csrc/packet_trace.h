@@ -415,24 +415,6 @@ __device__ __forceinline__ void enter_direction(const frame3f& f, vec3f wd, unsi
     ci = {1.0f / cd.x, 1.0f / cd.y, 1.0f / cd.z};
 }
 
-// transform_point_inverse(f, wo) (vmath.h:275-278: dot(f.x, wo - f.o), ...) for an instance
-// entry. With the rotation rows bitwise the identity's (`ident`), each dot is
-// ((1 * b.x + 0 * b.y) + 0 * b.z) (and its permutations) for b = wo - f.o, which is b's
-// component bit for bit when the three components are finite and none is -0 (a product 0 * v
-// is +-0, and c + +-0 == c except that -0 + +0 is +0): then the three subtractions are the
-// whole transform (3 VALU and one class test per component instead of 18). A wave in which a
-// lane of `lanes` has an infinite, NaN or -0 component takes the full transform.
-__device__ __forceinline__ vec3f enter_point(const frame3f& f, vec3f wo, bool ident, unsigned long long lanes) {
-    if (ident) {
-        const vec3f bo = wo - f.o;
-        constexpr int bad = 0x001 | 0x002 | 0x004 | 0x020 | 0x200;  // sNaN, qNaN, -inf, -0, +inf
-        const bool fast = !__builtin_amdgcn_class(bo.x, bad) && !__builtin_amdgcn_class(bo.y, bad) &&
-                          !__builtin_amdgcn_class(bo.z, bad);
-        if (!(ballot(!fast) & lanes)) return bo;
-    }
-    return transform_point_inverse(f, wo);
-}
-
 // intersect_check_bbox (scene.cpp:371-382) with the per-axis swap decided at compile
 // time: OCT bit a set = this lane's invd component a is < 0 (the reference's swap
 // condition). The same two products per axis are computed -- (lo - o) * invd and
@@ -826,8 +808,8 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     float4 fr[4];
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
+                    co = transform_point_inverse(f, wo);
                     const bool ident = (uniform(ibits(fr[0].w)) & (int)inst_identity_bit) != 0;
-                    co = enter_point(f, wo, ident, live & ~done);
                     if (ident)
                         cd = icd, ci = ici;
                     else
@@ -1122,26 +1104,12 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f 
 // ds_read_b128 at a wave-uniform address; every other record through the scalar cache.
 // `base`: the records `cur` is a byte offset into (S.wnodes, or a shadow bundle's list,
 // packet_occluded_wide2)
-//
-// root (after an instance entry): the shape root's own box, which the wide root record (its
-// children's boxes) skips, is tested first -- here, in the octant's copy, rather than with the
-// run-time swaps of box_hit6 at the entry (the same products, bit for bit); no passing lane:
-// mask = 0, the caller moves on to the next instance
-#ifndef YRT_ROOT_IN_DESCENT
-#define YRT_ROOT_IN_DESCENT 1
-#endif
 template <int OCT, int LDSN>
 __device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, vec3f co, vec3f ci,
                                              const inner_planes& P,
                                              float tmin, float tmax, uint32_t& cur, unsigned long long& mask,
                                              int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
-                                             unsigned long long done, unsigned& nsteps, bool& root,
-                                             const float (&rb)[6]) {
-    if (root) {
-        root = false;
-        mask &= ballot(box_oct<OCT>(co, ci, tmin, tmax, rb[0], rb[1], rb[2], rb[3], rb[4], rb[5]));
-        if (!mask) return;
-    }
+                                             unsigned long long done, unsigned& nsteps) {
     const f4* wbase = sgpr_ptr(base);
     for (;;) {
         bool more;
@@ -1205,9 +1173,6 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     const int ioct = wave_octant(ici, live);
     // the inner slots' conservative planes of the current level (recomputed with co / ci)
     inner_planes ip = make_inner_planes(wo, wi, live);
-    // an instance entry's shape root box, tested at the start of the next descent
-    bool root = false;
-    float rb[6] = {0, 0, 0, 0, 0, 0};
     unsigned nsteps0 = 0, nsteps1 = 0;
 #ifdef YRT_WIDE_STATS
     unsigned ws[16] = {1, 0, 0, 0, 0, 0, 0, 0};
@@ -1220,7 +1185,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                           sp < 61, 4, (int)cur, sp, level,
                       base, 0);
 #define YRT_WD(o) wide_descend<o, LDSN>(level ? S.wnodes : tbase, lds, co, ci, ip, tmin, tmax, cur, mask, sp, stk_word, \
-                                         stk_mlo, stk_mhi, wfloor, done, level ? nsteps1 : nsteps0, root, rb)
+                                         stk_mlo, stk_mhi, wfloor, done, level ? nsteps1 : nsteps0)
             switch (oct) {
                 case 0: YRT_WD(0); break;
                 case 1: YRT_WD(1); break;
@@ -1294,8 +1259,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     float4 fr[winst_rows];
                     ld_records_at<winst_rows>(S.winst, (unsigned)(winst_rows * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
+                    co = transform_point_inverse(f, wo);
                     const bool ident = (uniform(ibits(fr[0].w)) & (int)inst_identity_bit) != 0;
-                    co = enter_point(f, wo, ident, live & ~done);
                     if (ident)
                         cd = icd, ci = ici;
                     else
@@ -1304,15 +1269,11 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                     cur = rk & 0x3fffffffu;  // the shape's wide root (a record byte offset)
                     kind = (int)(rk >> 30);
                     mask = inst_mask & ~done;
-                    // the shape root's own box, which the wide root (its children's children)
-                    // skips: the reference tests it first, and a lane that fails it finds
-                    // nothing in this instance (every box below is inside it). Tested at the
-                    // start of the descent, in the octant's copy (wide_descend)
-                    if (YRT_ROOT_IN_DESCENT) {
-                        root = true;
-                        rb[0] = fr[2].w, rb[1] = fr[3].w, rb[2] = fr[4].x, rb[3] = fr[4].y, rb[4] = fr[4].z,
-                        rb[5] = fr[4].w;
-                    } else {
+                    {
+                        // the shape root's own box, which the wide root (its children's
+                        // children) skips: the reference tests it first, and a lane that
+                        // fails it finds nothing in this instance (every box below is
+                        // inside it)
                         float tn;
                         mask &= ballot(box_hit6(co, ci, tmin, tmax, fr[2].w, fr[3].w, fr[4].x, fr[4].y, fr[4].z,
                                                 fr[4].w, tn));
