@@ -17,7 +17,7 @@ from ab_variants import bind  # noqa: E402
 import torch  # noqa: E402
 
 NAMES = ["walks", "steps_top", "steps_shape", "inst_entries", "leaves", "prim_tests", "pops", "empty_pops",
-         "live_lanes", "occluded_lanes", "walks_all_occluded", "steps_in_all_occluded", "-", "-", "-", "-"]
+         "live_lanes", "occluded_lanes", "walks_all_occluded", "steps_in_all_occluded", "entries_root_missed", "-", "-", "-"]
 
 
 def main():

@@ -1279,6 +1279,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                                                 fr[4].w, tn));
                     }
                     WSTAT(3, 1u);
+                    WSTAT(12, mask ? 0u : 1u);  // entries whose root box no lane passes
                     oct = ident ? ioct : wave_octant(ci, live & ~done);
                     ip = make_inner_planes(co, ci, mask);
                     if (mask) break;
@@ -1312,7 +1313,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     ws[10] = (live & ~done) ? 0u : 1u, ws[11] = (live & ~done) ? 0u : nsteps0 + nsteps1;
     if (__lane_id() == 0) {
         unsigned long long* line = g_wide_stats + 16 * ((blockIdx.x * 7u + threadIdx.x / 64u) & 1023u);
-        for (int i = 0; i < 12; i++) atomicAdd(line + i, (unsigned long long)ws[i]);
+        for (int i = 0; i < 13; i++) atomicAdd(line + i, (unsigned long long)ws[i]);
     }
 #endif
     return (done & me) != 0;
