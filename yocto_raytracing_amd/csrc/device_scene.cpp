@@ -14,6 +14,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -459,6 +460,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
 
     // ---- instance level: nodes + instances permuted into leaf order ----
     std::vector<f4> tnodes, tinst, winst;
+    std::vector<std::array<double, 6>> iboxd;  // per instance slot: its world box (lo, hi), no margin
     std::vector<int> tinst_id;
     for (auto& n : scn.bvh.nodes) {
         tnodes.push_back(node_lo(n, n.start));
@@ -600,6 +602,83 @@ device_scene* device_scene_create(const scene& scn, int device) {
         winst.push_back({t[2].x, t[2].y, t[2].z, rb.min.x});
         winst.push_back({t[3].x, t[3].y, t[3].z, rb.min.y});
         winst.push_back({rb.min.z, rb.max.x, rb.max.y, rb.max.z});
+        // the instance's world box (dev_scene_view ibox): the points w whose instance-space
+        // image transform_point_inverse(f, w) = R^T (w - o) lies in the root box are
+        // o + (R^T)^-1 l, so the root box's corners go through (R^T)^-1, in double (the margin
+        // is added below, once the scene's extent is known). Only for a frame whose axes are
+        // orthonormal to 2^-20: the walks reuse the world tmax as the instance-space tmax
+        // along the renormalised local direction, so a scaled frame stretches the segment a
+        // ray tests in its space (vmath.h:275-278); those instances keep NaN boxes, which no
+        // plane separates
+        {
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            const double R[3][3] = {{f.x.x, f.y.x, f.z.x}, {f.x.y, f.y.y, f.z.y}, {f.x.z, f.y.z, f.z.z}};  // columns: axes
+            bool ortho = true;
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    double g = 0.0;  // (R^T R)_ij
+                    for (int k = 0; k < 3; k++) g += R[k][i] * R[k][j];
+                    ortho = ortho && std::fabs(g - (i == j ? 1.0 : 0.0)) <= std::ldexp(1.0, -20);
+                }
+            const double det = R[0][0] * (R[1][1] * R[2][2] - R[1][2] * R[2][1]) -
+                               R[0][1] * (R[1][0] * R[2][2] - R[1][2] * R[2][0]) +
+                               R[0][2] * (R[1][0] * R[2][1] - R[1][1] * R[2][0]);
+            double Mi[3][3];  // (R^T)^-1 = the cofactor matrix of R over det(R)
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+                    Mi[i][j] = (R[i1][j1] * R[i2][j2] - R[i1][j2] * R[i2][j1]) / det;
+                }
+            const bool empty = !(rb.min.x <= rb.max.x && rb.min.y <= rb.max.y && rb.min.z <= rb.max.z);
+            const bool nan = std::isnan(rb.min.x) || std::isnan(rb.min.y) || std::isnan(rb.min.z) ||
+                             std::isnan(rb.max.x) || std::isnan(rb.max.y) || std::isnan(rb.max.z) || !ortho ||
+                             !std::isfinite(det) || !std::isfinite(f.o.x) || !std::isfinite(f.o.y) ||
+                             !std::isfinite(f.o.z);
+            if (nan) {
+                for (int a = 0; a < 3; a++) lo[a] = hi[a] = NAN;
+            } else if (!empty) {
+                const double o[3] = {f.o.x, f.o.y, f.o.z};
+                for (int c = 0; c < 8; c++) {
+                    const double l[3] = {(c & 1) ? rb.max.x : rb.min.x, (c & 2) ? rb.max.y : rb.min.y,
+                                         (c & 4) ? rb.max.z : rb.min.z};
+                    for (int a = 0; a < 3; a++) {
+                        const double w = o[a] + Mi[a][0] * l[0] + Mi[a][1] * l[1] + Mi[a][2] * l[2];
+                        lo[a] = std::min(lo[a], w), hi[a] = std::max(hi[a], w);
+                    }
+                }
+            }
+            iboxd.push_back({lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
+        }
+    }
+    // the world boxes' margin: 2^-14 of four times the scene's extent (a bound on the list
+    // builders' points: hit points, lights and the camera of a usual view), ~1000x the
+    // rounding of an instance transform and slab test at that scale; the builders' own
+    // cone / hull margins (1e-3 + 3e-5 of their coordinates) come on top
+    std::vector<f4> ibox;
+    {
+        double M = 0.0;
+        for (auto& b : iboxd)
+            for (double c : b)
+                if (std::isfinite(c)) M = std::max(M, std::fabs(c));
+        const double eps = (4.0 * M + 1.0) * std::ldexp(1.0, -14);
+        auto down = [](double x) {
+            float v = (float)x;
+            if ((double)v > x) v = std::nextafter(v, -INFINITY);
+            return v;
+        };
+        auto up = [](double x) {
+            float v = (float)x;
+            if ((double)v < x) v = std::nextafter(v, INFINITY);
+            return v;
+        };
+        for (auto& b : iboxd) {
+            f4 lo = {down(b[0] - eps), down(b[1] - eps), down(b[2] - eps), 0.0f};
+            f4 hi = {up(b[3] + eps), up(b[4] + eps), up(b[5] + eps), 0.0f};
+            for (int a = 0; a < 6; a++)
+                if (std::isnan(b[a])) lo = {NAN, NAN, NAN, 0.0f}, hi = {NAN, NAN, NAN, 0.0f};
+            ibox.push_back(lo);
+            ibox.push_back(hi);
+        }
     }
 
     // ---- materials, lights, textures ----
@@ -677,6 +756,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_trel = ab.add(tpair.data(), tpair.size() * sizeof(f4));  // rewritten per render
     size_t o_spair = ab.add(spair.data(), spair.size() * sizeof(f4));
     size_t o_tinst_id = ab.add(tinst_id.data(), tinst_id.size() * sizeof(int));
+    size_t o_ibox = ab.add(ibox.data(), ibox.size() * sizeof(f4));
 
     try {
         check(hipSetDevice(device), "hipSetDevice");
@@ -721,6 +801,8 @@ device_scene* device_scene_create(const scene& scn, int device) {
     ds->trel = (f4*)(base + o_trel);
     v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);
+    v.ibox = ibox.empty() ? nullptr : (const f4*)(base + o_ibox);
+    v.inst_masks = !ibox.empty() && tinst.size() / 4 < ((size_t)1 << 21) ? 1 : 0;
     v.wtop_root = wtop_root * wide_record_bytes;
     v.nwtop = wtop_records;
     v.wide = ds->wide_ok ? 1 : 0;

@@ -619,6 +619,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0, mask = live;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
+    uint32_t inst_skip = 0;  // bit i: skip the current leaf's next instance i (camera list cones)
     int node = 0;  // byte offset of the current spine record from pbase
     const f4* const ptop = REL ? trel : S.tpair;
     const f4* pbase = ptop;
@@ -745,6 +746,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 inst_next = lstart;
                 inst_end = lstart + lcount;
                 inst_mask = lmask;
+                // a camera list's leaf: the instances its tile's cone excludes (bits 16-30 of
+                // the count word, wavefront.hip k_camera_lists); a tree leaf: none
+                inst_skip = (lcl >> 16) & 0x7fffu;
                 level = 1;
                 base = sp;
             } else {
@@ -803,7 +807,16 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
             if (level == 1 && sp == base) {
                 if (inst_next < inst_end) {
                     // enter instance k: transform_ray_inverse (vmath.h:275-278), every lane
+                    if (inst_skip) {
+                        // the instances the tile's cone excludes (no lane passes their root
+                        // box) are passed over: the run of skip bits at the bottom
+                        const int z = __builtin_ctz(~inst_skip);
+                        inst_next += z;
+                        inst_skip >>= z;
+                        if (inst_next >= inst_end) continue;
+                    }
                     const int k = inst_next++;
+                    inst_skip >>= 1;
                     DBG_CHECK(k >= 0 && k < S.ninst, 3, k, inst_end, sp, base, 0);
                     float4 fr[4];
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
@@ -1158,7 +1171,10 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     int stk_word = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
+    uint32_t inst_skip = 0;  // bit i: skip the current leaf's next instance i (bundle hulls)
     if (!tbase) tbase = S.wnodes, troot = (uint32_t)S.wtop_root;
+    // level 0 walks a shadow bundle's list in the bundle records' leaf format
+    const bool blist = S.inst_masks && tbase != S.wnodes;
     // the current item: a child word (a wide node's byte offset, or a leaf)
     uint32_t cur = troot;
     unsigned long long mask = live;
@@ -1204,8 +1220,11 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             const int first = (int)(cur & wide_index_mask);
             const int count = (int)((cur >> wide_count_shift) & 7u);
             if (level == 0) {
-                inst_next = first;
-                inst_end = first + count;
+                // a shadow bundle's leaf (bundle_leaf_word): the instances its hull excludes
+                // are skipped (wavefront.hip k_bundle_lists); a tree leaf: none
+                inst_next = blist ? (int)(cur & bundle_first_mask) : first;
+                inst_skip = blist ? (cur >> bundle_skip_shift) & 0x7fu : 0u;
+                inst_end = inst_next + count;
                 inst_mask = mask;
                 level = 1;
                 base = sp;
@@ -1254,7 +1273,16 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
         for (;;) {
             if (level == 1 && sp == base) {
                 if (inst_next < inst_end) {
+                    if (inst_skip) {
+                        // the instances the bundle's hull excludes (no lane passes their root
+                        // box) are passed over: the run of skip bits at the bottom
+                        const int z = __builtin_ctz(~inst_skip);
+                        inst_next += z;
+                        inst_skip >>= z;
+                        if (inst_next >= inst_end) continue;
+                    }
                     const int k = inst_next++;
+                    inst_skip >>= 1;
                     DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_end, sp, base, 0);
                     float4 fr[winst_rows];
                     ld_records_at<winst_rows>(S.winst, (unsigned)(winst_rows * k), fr);

@@ -481,6 +481,11 @@ static_assert(bundle_g >= 1 && bundle_g <= 64, "one item per lane of k_bundle_li
 // hit points' centre (their own instance) last: 11.71 / 7.39
 #define YRT_BUNDLE_SORT 2
 #endif
+#ifndef YRT_INSTANCE_MASKS
+// the list builders mark the instances of a listed leaf that their cone / hull excludes, and
+// the walks skip them (k_camera_lists, k_bundle_lists; dev_scene_view ibox)
+#define YRT_INSTANCE_MASKS 1
+#endif
 constexpr int bundle_max = 16;        // candidate leaves per list
 constexpr int bundle_recs = 5;        // wide records per list: a chain (3 + 3 + 3 + 3 + 4 leaves)
 constexpr int bundle_max_lights = 8;  // more lights: no bundles (the lists' memory grows with them)
@@ -1263,6 +1268,31 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
             for (int q = 0; q < 7; q++) cand[w][rank][q] = e[q];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    // the instances of each listed leaf that the hull excludes: their world boxes
+    // (dev_scene_view ibox) outside a hull plane by more than the margin fail every ray's
+    // root box test in the instance's space, so the walk skips them (skip bits in the leaf's
+    // word: the bundle records' format, bundle_leaf_word)
+    if (YRT_INSTANCE_MASKS && S.inst_masks) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int e = 0; e < nc; e++) {
+            const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(cand[w][e][6]));
+            const int first = (int)(wu & wide_index_mask), count = (int)((wu >> wide_count_shift) & 7u);
+            uint32_t skip = 0;
+            for (int i0 = 0; count > 1 && i0 < count; i0 += 4) {
+                const int i = i0 + (lane >> 4);  // lane 16 s + j: instance i0 + s against plane j
+                bool sep = false;
+                if (i < count) {
+                    const float4 a = ld4(S.ibox + 2 * (first + i)), b = ld4(S.ibox + 2 * (first + i) + 1);
+                    sep = hull_sep(H, a.x, a.y, a.z, b.x, b.y, b.z);
+                }
+                const unsigned long long sm = ballot(sep);
+                for (int q = 0; q < 4; q++)
+                    if (i0 + q < count && ((sm >> (16 * q)) & 0xffffull)) skip |= 1u << (i0 + q);
+            }
+            if (lane == 0) cand[w][e][6] = __uint_as_float(bundle_leaf_word(first, count, skip));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     // the list as wide records at B.lists + gl * bundle_recs: up to 4 leaves in the root;
     // more in up to 4 child records of 4, the root's slot c holding child c's box (the union
     // of its leaves' boxes) and its byte offset from B.lists
@@ -1436,7 +1466,24 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane < nf) {
         f4* out = B.clist + ((size_t)t * camera_list_max + lane) * 2;
-        const float4 lo = fr[w][cur][lane][0], hi = fr[w][cur][lane][1];
+        const float4 lo = fr[w][cur][lane][0];
+        float4 hi = fr[w][cur][lane][1];
+        // a listed leaf's instances that the cone excludes (their world boxes, dev_scene_view
+        // ibox, relative to O and outside a cone plane by more than the margin: every ray of
+        // the tile fails their root box test in the instance's space): skip bits 16-30 of the
+        // entry's count word, which packet_first's list mode honours (a tree leaf's are 0)
+        const uint32_t cw = ubits(hi.w);
+        const int count = (int)(cw & 0xffffu);
+        if (YRT_INSTANCE_MASKS && S.ibox && (cw & leaf_bit) && count > 1 && count <= 15) {
+            const int first = ibits(lo.w);
+            uint32_t skip = 0;
+            for (int i = 0; i < count; i++) {
+                const float4 a = ld4(S.ibox + 2 * (first + i)), b = ld4(S.ibox + 2 * (first + i) + 1);
+                const float4 ar = {a.x - O.x, a.y - O.y, a.z - O.z, 0.0f}, br = {b.x - O.x, b.y - O.y, b.z - O.z, 0.0f};
+                if (outside(ar, br)) skip |= 1u << i;
+            }
+            hi.w = __uint_as_float(cw | skip << 16);
+        }
         out[0] = {lo.x, lo.y, lo.z, lo.w};
         out[1] = {hi.x, hi.y, hi.z, hi.w};
     }

@@ -74,6 +74,14 @@ constexpr uint32_t wide_leaf = 0x80000000u;
 constexpr int wide_count_shift = 28;
 constexpr uint32_t wide_index_mask = 0x0fffffffu;
 constexpr int wide_record_bytes = 128;
+// a shadow bundle's leaf word (wavefront.hip k_bundle_lists, when the view's inst_masks is
+// set): wide_leaf | count << 28 | skip << 21 | first slot, skip bit i = the leaf's instance i
+// is excluded by the bundle's hull (first < 2^21)
+constexpr uint32_t bundle_first_mask = 0x1fffffu;
+constexpr int bundle_skip_shift = 21;
+constexpr uint32_t bundle_leaf_word(int first, int count, uint32_t skip) {
+    return wide_leaf | (uint32_t)count << wide_count_shift | (skip & 0x7fu) << bundle_skip_shift | (uint32_t)first;
+}
 constexpr int spine_len = 2;  // nodes per closest-hit walk record (a node and its child start+1)
 // spine records (tpair/spair): spine_len x {lo, hi} f4 pairs; an inner node's lo.w is
 // the byte offset of its child start's record (child start+1's is the next record)
@@ -102,6 +110,12 @@ struct dev_scene_view {
                       // child start+1's, that child's start+1's, ... (right spine)
     const f4* spair;  // the same for the shape BVHs (same indexing as snodes)
     const int* tinst_id;
+    // per instance slot: a world-space box holding every point whose instance-space image
+    // lies in the shape's root box, grown by a margin far above the rounding of the walks'
+    // instance transforms (device_scene.cpp), NaN for frames it cannot bound; the list
+    // builders drop the instances of a listed leaf that their cone or hull excludes
+    const f4* ibox;
+    int inst_masks;  // 1: instance slots fit the bundle records' 21-bit first-slot field
     int wtop_root;
     int nwtop;  // records of the instance-level wide tree (breadth first: the top levels lead)
     int wide;  // 1: any-hit queries use the 4-wide walk
