@@ -619,7 +619,6 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0, mask = live;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
-    uint32_t inst_skip = 0;  // bit i: skip the current leaf's next instance i (camera list cones)
     int node = 0;  // byte offset of the current spine record from pbase
     const f4* const ptop = REL ? trel : S.tpair;
     const f4* pbase = ptop;
@@ -746,9 +745,25 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 inst_next = lstart;
                 inst_end = lstart + lcount;
                 inst_mask = lmask;
-                // a camera list's leaf: the instances its tile's cone excludes (bits 16-30 of
-                // the count word, wavefront.hip k_camera_lists); a tree leaf: none
-                inst_skip = (lcl >> 16) & 0x7fffu;
+                if (LM) {
+                    // a camera list's leaf: the instances its tile's cone excludes (bits 16-30
+                    // of the count word, wavefront.hip k_camera_lists; a tree leaf's are 0).
+                    // The runs of them at either end of the leaf are dropped here, once per
+                    // leaf; one between kept instances is entered as before (its root box
+                    // test fails for every lane). (Skipping those too, per entry, cost the
+                    // closest hit more scalar work than it saved: c4 primary 9.42 -> 9.62 ms
+                    // with a keep mask, instance100k +1 ms.)
+                    const uint32_t skip = (lcl >> 16) & 0x7fffu;
+                    if (skip) {
+                        const uint32_t keep = ~skip & ((1u << lcount) - 1u);  // (count <= 15 when skip != 0)
+                        if (!keep) {
+                            inst_end = inst_next;
+                        } else {
+                            inst_next = lstart + __builtin_ctz(keep);
+                            inst_end = lstart + 32 - __builtin_clz(keep);
+                        }
+                    }
+                }
                 level = 1;
                 base = sp;
             } else {
@@ -807,16 +822,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
             if (level == 1 && sp == base) {
                 if (inst_next < inst_end) {
                     // enter instance k: transform_ray_inverse (vmath.h:275-278), every lane
-                    if (inst_skip) {
-                        // the instances the tile's cone excludes (no lane passes their root
-                        // box) are passed over: the run of skip bits at the bottom
-                        const int z = __builtin_ctz(~inst_skip);
-                        inst_next += z;
-                        inst_skip >>= z;
-                        if (inst_next >= inst_end) continue;
-                    }
                     const int k = inst_next++;
-                    inst_skip >>= 1;
                     DBG_CHECK(k >= 0 && k < S.ninst, 3, k, inst_end, sp, base, 0);
                     float4 fr[4];
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
@@ -1170,8 +1176,10 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     vec3f co = wo, cd = wd, ci = wi;
     int stk_word = 0, stk_mlo = 0, stk_mhi = 0;
     unsigned long long done = 0, inst_mask = 0;
-    int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0;
-    uint32_t inst_skip = 0;  // bit i: skip the current leaf's next instance i (bundle hulls)
+    int level = 0, sp = 0, base = 0, kind = 0, inst_first = 0;
+    // the current leaf's instances still to enter: bit i = instance inst_first + i (a wide leaf
+    // holds at most 7); the instances a bundle's hull excludes are not in it (its skip bits)
+    uint32_t inst_keep = 0;
     if (!tbase) tbase = S.wnodes, troot = (uint32_t)S.wtop_root;
     // level 0 walks a shadow bundle's list in the bundle records' leaf format
     const bool blist = S.inst_masks && tbase != S.wnodes;
@@ -1222,9 +1230,8 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             if (level == 0) {
                 // a shadow bundle's leaf (bundle_leaf_word): the instances its hull excludes
                 // are skipped (wavefront.hip k_bundle_lists); a tree leaf: none
-                inst_next = blist ? (int)(cur & bundle_first_mask) : first;
-                inst_skip = blist ? (cur >> bundle_skip_shift) & 0x7fu : 0u;
-                inst_end = inst_next + count;
+                inst_first = blist ? (int)(cur & bundle_first_mask) : first;
+                inst_keep = ((1u << count) - 1u) & ~(blist ? (cur >> bundle_skip_shift) & 0x7fu : 0u);
                 inst_mask = mask;
                 level = 1;
                 base = sp;
@@ -1272,18 +1279,10 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
         bool finished = false;
         for (;;) {
             if (level == 1 && sp == base) {
-                if (inst_next < inst_end) {
-                    if (inst_skip) {
-                        // the instances the bundle's hull excludes (no lane passes their root
-                        // box) are passed over: the run of skip bits at the bottom
-                        const int z = __builtin_ctz(~inst_skip);
-                        inst_next += z;
-                        inst_skip >>= z;
-                        if (inst_next >= inst_end) continue;
-                    }
-                    const int k = inst_next++;
-                    inst_skip >>= 1;
-                    DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_end, sp, base, 0);
+                if (inst_keep) {
+                    const int k = inst_first + __builtin_ctz(inst_keep);
+                    inst_keep &= inst_keep - 1u;
+                    DBG_CHECK(k >= 0 && k < S.ninst, 6, k, inst_first, sp, base, 0);
                     float4 fr[winst_rows];
                     ld_records_at<winst_rows>(S.winst, (unsigned)(winst_rows * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};

@@ -1292,6 +1292,24 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
             if (lane == 0) cand[w][e][6] = __uint_as_float(bundle_leaf_word(first, count, skip));
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // a leaf whose every instance is excluded leaves the list (the walk would test its box
+        // and enter nothing); the others keep their order
+        float e[7] = {};
+        bool keep = false;
+        if (lane < nc) {
+            for (int q = 0; q < 7; q++) e[q] = cand[w][lane][q];
+            const uint32_t wu = ubits(e[6]);
+            const int count = (int)((wu >> wide_count_shift) & 7u);
+            const uint32_t all = (1u << count) - 1u;
+            keep = count == 0 || ((wu >> bundle_skip_shift) & 0x7fu) != all;
+        }
+        const unsigned long long km = ballot(keep);
+        const int pos = __popcll(km & ((1ull << lane) - 1ull));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads, before the writes
+        if (keep)
+            for (int q = 0; q < 7; q++) cand[w][pos][q] = e[q];
+        nc = __popcll(km);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     // the list as wide records at B.lists + gl * bundle_recs: up to 4 leaves in the root;
     // more in up to 4 child records of 4, the root's slot c holding child c's box (the union
@@ -1464,8 +1482,9 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
         cur ^= 1;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float4 elo = {0, 0, 0, 0}, ehi = {0, 0, 0, 0};
+    bool keep = false;
     if (lane < nf) {
-        f4* out = B.clist + ((size_t)t * camera_list_max + lane) * 2;
         const float4 lo = fr[w][cur][lane][0];
         float4 hi = fr[w][cur][lane][1];
         // a listed leaf's instances that the cone excludes (their world boxes, dev_scene_view
@@ -1483,10 +1502,21 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
                 if (outside(ar, br)) skip |= 1u << i;
             }
             hi.w = __uint_as_float(cw | skip << 16);
+            // a leaf whose every instance is excluded leaves the list
+            keep = skip != (1u << count) - 1u;
+        } else {
+            keep = true;
         }
-        out[0] = {lo.x, lo.y, lo.z, lo.w};
-        out[1] = {hi.x, hi.y, hi.z, hi.w};
+        elo = lo, ehi = hi;
     }
+    // the kept entries, in order
+    const unsigned long long km = ballot(keep);
+    if (keep) {
+        f4* out = B.clist + ((size_t)t * camera_list_max + __popcll(km & below)) * 2;
+        out[0] = {elo.x, elo.y, elo.z, elo.w};
+        out[1] = {ehi.x, ehi.y, ehi.z, ehi.w};
+    }
+    nf = __popcll(km);
     if (lane == 0) B.ccount[t] = nf;
 }
 
