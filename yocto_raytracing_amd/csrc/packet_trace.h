@@ -378,6 +378,10 @@ __device__ __forceinline__ bool dbg_fail(unsigned code, int a, int b, int c, int
 // entries, leaves reached in shapes, primitive tests, pops, empty pops, live lanes,
 // occluded lanes, walks that end with every live lane occluded, their steps}
 static __device__ unsigned long long g_wide_stats[1024 * 16];
+// the closest-hit walk's (packet_first, timed instantiations): per walk {walks, list
+// entries tested, spine records, instance entries, entries whose root record no lane passes,
+// shape leaves, primitive tests, pops, live lanes, hit lanes}
+static __device__ unsigned long long g_first_stats[1024 * 16];
 #define WSTAT(i, v) (ws[i] += (v))
 #else
 #define WSTAT(i, v) ((void)0)
@@ -510,6 +514,12 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         const bool p0 = box_oct<OCT>(bo, ci, tmin, tmax, rec[0].x, rec[0].y, rec[0].z, rec[1].x, rec[1].y, rec[1].z);
         const bool p1 = box_oct<OCT>(bo, ci, tmin, tmax, rec[2].x, rec[2].y, rec[2].z, rec[3].x, rec[3].y, rec[3].z);
         if (COUNT && (me & 1)) wc.wnode++;
+#ifdef YRT_WIDE_STATS
+        if (!COUNT) {
+            wc.wnode++;
+            if (!REL && node == 0 && !(ballot(p0) & mask)) wc.wprim++;  // (a shape's root record, REL callers)
+        }
+#endif
         if (COUNT && (mask & me)) wc.box++;
         const unsigned long long pm0 = ballot(p0) & mask;
         mask = pm0;
@@ -662,6 +672,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     float4 e[2];
                     ld_records_at<2>(lb, (unsigned)(2 * lnext), e);
                     lnext++;
+#ifdef YRT_WIDE_STATS
+                    wc.tex++;  // (stats build: list entries tested)
+#endif
                     const unsigned long long lanes = live & ~done;
                     unsigned long long m;
                     switch (oct) {
@@ -770,6 +783,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 const bool in = YRT_R5_LANE ? ((lmask >> lane_now()) & 1ull) != 0 : (lmask & me) != 0;
                 int leaf_hit = 0;
                 DBG_CHECK(lstart >= 0 && lstart + lcount <= S.nsprims, 2, lstart, lcount, level, kind, sp);
+#ifdef YRT_WIDE_STATS
+                if (!COUNT) wc.box++, wc.prim += (unsigned)lcount;  // (stats build: shape leaves, primitive tests)
+#endif
                 if (kind == kind_triangles) {
                     for (int i = lstart; i < lstart + lcount; i++) {
                         float4 pv[3];
@@ -824,6 +840,9 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     // enter instance k: transform_ray_inverse (vmath.h:275-278), every lane
                     const int k = inst_next++;
                     DBG_CHECK(k >= 0 && k < S.ninst, 3, k, inst_end, sp, base, 0);
+#ifdef YRT_WIDE_STATS
+                    if (!COUNT) wc.inst++;
+#endif
                     float4 fr[4];
                     ld_records_at<4>(S.tinst, (unsigned)(4 * k), fr);
                     const frame3f f = {xyz(fr[0]), xyz(fr[1]), xyz(fr[2]), xyz(fr[3])};
@@ -870,6 +889,18 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
             lstep = true;  // this list entry is done: the next one
         }
     }
+#ifdef YRT_WIDE_STATS
+    if (!COUNT) {
+        const unsigned long long hitl = ballot(hslot >= 0) & live;
+        if ((threadIdx.x & 63) == 0) {
+            unsigned long long* line = g_first_stats + 16 * ((blockIdx.x * 7u + threadIdx.x / 64u) & 1023u);
+            const unsigned long long v[10] = {1, wc.tex, wc.wnode, wc.inst, wc.wprim, wc.box, wc.prim, 0,
+                                              (unsigned long long)__popcll(live), (unsigned long long)__popcll(hitl)};
+            for (int i = 0; i < 10; i++) atomicAdd(line + i, v[i]);
+        }
+        wc = work_counts{};  // (a persistent caller keeps one wc across its items)
+    }
+#endif
     if (hslot < 0) return false;
     hr.slot = hslot;
     hr.ei = hei;

@@ -2324,6 +2324,22 @@ extern "C" int yrt_debug_wide_stats(unsigned long long* out16, int reset) {
 }
 #endif
 
+#ifdef YRT_WIDE_STATS
+extern "C" int yrt_debug_first_stats(unsigned long long* out16, int reset) {
+    static unsigned long long h[1024 * 16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(yrt::g_first_stats), sizeof h) != hipSuccess) return -1;
+    for (int i = 0; i < 16; i++) {
+        out16[i] = 0;
+        for (int k = 0; k < 1024; k++) out16[i] += h[16 * k + i];
+    }
+    if (reset) {
+        static const unsigned long long z[1024 * 16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_first_stats), z, sizeof z);
+    }
+    return 0;
+}
+#endif
+
 #ifdef YRT_TAIL_STATS
 // out: 8192 x {start, end, items, xcd} for kernel k (0 k_primary_persist, 1 k_shadow_persist)
 extern "C" int yrt_debug_tail(unsigned long long* out, int k) {
