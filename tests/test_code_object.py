@@ -22,7 +22,7 @@ LIB = ROOT / "yocto_raytracing_amd" / "libyrt.so"
 TIMED = {
     "k_primary_persist<uint, 0, list> (c4 closest hit)": (r"k_primary_persistIjLi0ELb1EE", 0, 0, 32),
     "k_primary_persist<uint, 0, tree> (lists off)": (r"k_primary_persistIjLi0ELb0EE", 0, 0, 32),
-    "k_shadow_persist<0> (c4 any hit)": (r"k_shadow_persistILi0EE", 0, 20, 32),
+    "k_shadow_persist<0> (c4 any hit)": (r"k_shadow_persistILi0EE", 0, 0, 32),
     "k_shade<fused, occ4> (c4 shading + per-pixel sum)": (r"k_shadeILb0ELb1ELi256ELb1EE", 0, 0, 32),
     "k_shade<level, occ4> (c3 mirror levels)": (r"k_shadeILb0ELb0ELi256ELb1EE", 0, 0, 64),
     "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 40),
