@@ -1197,16 +1197,18 @@ __device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, 
 template <int LDSN = 0>
 __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid,
                                                       const float4* lds = nullptr, const f4* tbase = nullptr,
-                                                      uint32_t troot = 0) {
+                                                      uint32_t troot = 0, unsigned long long pre_done = 0) {
     const unsigned long long me = 1ull << __lane_id();
     const unsigned long long live = ballot(valid && !is_nan(wray.tmin) && !is_nan(wray.tmax));
     if (!live) return false;
+    // pre_done: lanes answered already (their shadow ray is culled: reported occluded)
+    if (!(live & ~pre_done)) return (pre_done & me) != 0;
     const vec3f wo = wray.o, wd = wray.d;
     const vec3f wi = rcp3(wd, live);
     const float tmin = wray.tmin, tmax = wray.tmax;
     vec3f co = wo, cd = wd, ci = wi;
     int stk_word = 0, stk_mlo = 0, stk_mhi = 0;
-    unsigned long long done = 0, inst_mask = 0;
+    unsigned long long done = pre_done & live, inst_mask = 0;
     int level = 0, sp = 0, base = 0, kind = 0, inst_first = 0;
     // the current leaf's instances still to enter: bit i = instance inst_first + i (a wide leaf
     // holds at most 7); the instances a bundle's hull excludes are not in it (its skip bits)
@@ -1216,7 +1218,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
     const bool blist = S.inst_masks && tbase != S.wnodes;
     // the current item: a child word (a wide node's byte offset, or a leaf)
     uint32_t cur = troot;
-    unsigned long long mask = live;
+    unsigned long long mask = live & ~done;
     // the octant of the current level's rays when the whole wave shares it (8: mixed)
     const int woct = wave_octant(wi, live);
     int oct = woct;

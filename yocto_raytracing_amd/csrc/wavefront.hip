@@ -1636,13 +1636,15 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
             }
         }
         rays += (unsigned)__popcll(ballot(valid));
-        // a wave whose every ray has a zero light term skips the walk (per-lane culling inside
-        // this loop trips the compiler: "illegal VGPR to SGPR copy"; the 64 rays of a wave are
-        // one pixel's samples at c4, so they agree). light_term_zero runs in uniform control
-        // flow: its loads and ballots on every lane.
-        const bool all_culled =
-            YRT_SHADOW_CULL && !YRT_HIT16 &&
-            !ballot(valid && !light_term_zero(info, xyz(s1), sr.o, cam_o, sr.d, r, xyz(lrec[5])));
+        // the rays whose light term is zero (light_term_zero, in uniform control flow: its loads
+        // and ballots on every lane) start the walk as done -- recorded as occluded -- and a
+        // wave whose every ray is culled skips it. (Taking them out of `valid` instead trips the
+        // compiler inside this loop: "illegal VGPR to SGPR copy".)
+        const unsigned long long culled =
+            (YRT_SHADOW_CULL && !YRT_HIT16) ? ballot(valid && light_term_zero(info, xyz(s1), sr.o, cam_o, sr.d, r,
+                                                                                xyz(lrec[5])))
+                                             : 0ull;
+        const bool all_culled = YRT_SHADOW_CULL && !YRT_HIT16 && culled == ballot(valid);
         bool occ;
         int lc = -1;  // the bundle's list: its leaf count, -1 = walk the tree
         if (YRT_SHADOW_BUNDLES && LDSN == 0 && B.bundles) {
@@ -1657,7 +1659,9 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         }
         // lc == 0: no leaf can be passed by these rays, none is occluded; all_culled: recorded
         // as occluded, k_shade skips the light
-        occ = all_culled ? true : lc == 0 ? false : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot);
+        occ = all_culled ? true
+                         : lc == 0 ? ((culled >> lane) & 1ull) != 0
+                                   : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot, culled);
         if (valid) stb(B.occl + (size_t)li * B.capacity + idx, occ ? 1 : 0);
     }
 #ifdef YRT_TAIL_STATS
