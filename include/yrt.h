@@ -197,12 +197,13 @@ int yrt_trace_any(yrt_scene* ds, const float* rays, int n, unsigned char* hit, i
  * YRT_ALGO_MEGAKERNEL / YRT_ALGO_WAVEFRONT_LANE = one independent walk per lane */
 int yrt_scene_set_trace_algorithm(yrt_scene* ds, int algorithm);
 /* per-tile candidate lists of yrt_render (camera frontier lists and shadow
- * bundles; identical images either way): YRT_LISTS_AUTO (default) and YRT_LISTS_ON build them
- * whenever the scene allows (an instance tree of >= 8 wide records; shadow bundles for at
- * most 8 lights, a rotated light's rays walking the tree; ON also runs level 0's shadow rays
- * on the persistent grid at any frame size), YRT_LISTS_OFF never builds them. No mode reads
- * anything back during a render. Set it between renders of the handle, not while one is in
- * flight. */
+ * bundles; identical images either way): YRT_LISTS_ON builds them whenever the scene allows
+ * (an instance tree of >= 8 wide records; shadow bundles for at most 8 lights, a rotated
+ * light's rays walking the tree; ON also runs level 0's shadow rays on the persistent grid at
+ * any frame size), YRT_LISTS_AUTO (default) does the same from 9 samples per pixel (their
+ * cost is per pixel tile, their gain per sample), YRT_LISTS_OFF never builds them. No mode
+ * reads anything back during a render. Set it between renders of the handle, not while one
+ * is in flight. */
 int yrt_scene_set_tile_lists(yrt_scene* ds, int mode);
 /* the lists' state after the last yrt_render on this handle (synchronises with it):
  * whether each kind is in use, and sums[4] = {camera-list entries, camera lists, bundle-list

@@ -101,6 +101,17 @@ def test_lists_auto(yrt):
         del ds
 
 
+def test_lists_auto_by_samples(yrt):
+    """auto builds the lists from 9 samples per pixel (YRT_LISTS_MIN_SPP: their cost is per
+    pixel tile, their gain per sample); below that it renders without them, the same image"""
+    ds = host(yrt, "instance10000").upload(0)
+    for s, used in ((1, False), (2, False), (3, True)):
+        auto, _, la = render(yrt, ds, "auto", 180, s)
+        assert la["camera"] == used, (s, la)
+        on, _, _ = render(yrt, ds, "on", 180, s)
+        np.testing.assert_array_equal(auto.view(np.uint32), on.view(np.uint32))
+
+
 def _grid_scene(yrt, tmp_path, nlights, rotated_light):
     """16 x 16 boxes on a floor (an instance tree of well over 8 wide records) lit by point
     lights; optionally one light's frame rotated (its shadow rays leave p along

@@ -52,6 +52,7 @@ VARIANTS = {
     "YRT_ANY_CONSERVATIVE": ["-DYRT_ANY_CONSERVATIVE=1"],
     "YRT_SHADOW_CULL": ["-DYRT_SHADOW_CULL=0"],
     "YRT_INSTANCE_MASKS": ["-DYRT_INSTANCE_MASKS=0"],
+    "YRT_LISTS_MIN_SPP": ["-DYRT_LISTS_MIN_SPP=1"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change
     "YRT_R5_LANE": ["-DYRT_R5_LANE=0", "-DYRT_R5_UORIG=0", "-DYRT_R5_VCONST=0", "-DYRT_R5_IDXLANE=0", "-DYRT_R5_SURF=0"],
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],

@@ -182,8 +182,9 @@ class DeviceScene:
         check(N.lib.yrt_scene_set_trace_algorithm(self._h, ALGORITHMS[algorithm]), "set_trace_algorithm")
 
     def set_tile_lists(self, mode: str) -> None:
-        """per-tile candidate lists of render_into: "auto" (default) and "on" build them whenever
-        the scene allows, "off" never -- identical images either way"""
+        """per-tile candidate lists of render_into: "on" builds them whenever the scene allows,
+        "auto" (default) the same from 9 samples per pixel, "off" never -- identical images
+        either way"""
         check(N.lib.yrt_scene_set_tile_lists(self._h, TILE_LISTS[mode]), "set_tile_lists")
 
     def tile_lists(self) -> dict:

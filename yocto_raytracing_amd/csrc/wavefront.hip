@@ -481,6 +481,14 @@ static_assert(bundle_g >= 1 && bundle_g <= 64, "one item per lane of k_bundle_li
 // hit points' centre (their own instance) last: 11.71 / 7.39
 #define YRT_BUNDLE_SORT 2
 #endif
+#ifndef YRT_LISTS_MIN_SPP
+// the lists' cost is per 8x8-pixel tile (~0.2 ms at 1080p), their gain per sample: in one
+// process (profiles/r5/ab/r5t_*) instance10000 at 1080p with lists on / off -- 1 spp 1.79 /
+// 1.54 ms, 4 spp 3.00 / 3.06, 16 spp 6.84 / 7.93, 64 spp 19.41 / 24.18; instance100k at 4 spp
+// 4.21 / 3.99, instance1k 1.50 / 1.65. YRT_LISTS_AUTO builds them from this many samples per
+// pixel (a 3x3 grid)
+#define YRT_LISTS_MIN_SPP 9
+#endif
 #ifndef YRT_INSTANCE_MASKS
 // the list builders mark the instances of a listed leaf that their cone / hull excludes, and
 // the walks skip them (k_camera_lists, k_bundle_lists; dev_scene_view ibox)
@@ -2138,9 +2146,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         // the camera rays walk their tiles' leaf lists (k_camera_lists)
         const bool cam_lists_possible = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
                                         ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
-        // (YRT_LISTS_AUTO / _ON: whenever the scene allows; _OFF: never -- yrt_scene_set_tile_lists)
-        B.cam_lists = cam_lists_possible && ds.lists_mode != 2;
-        B.bundles = bundles_possible && ds.lists_mode != 2;
+        // YRT_LISTS_ON: whenever the scene allows; YRT_LISTS_AUTO: the same from
+        // YRT_LISTS_MIN_SPP samples per pixel; _OFF: never (yrt_scene_set_tile_lists)
+        const bool lists = ds.lists_mode == 1 || (ds.lists_mode == 0 && spp >= YRT_LISTS_MIN_SPP);
+        B.cam_lists = cam_lists_possible && lists;
+        B.bundles = bundles_possible && lists;
         ds.last_camera_lists |= B.cam_lists != 0, ds.last_bundles |= B.bundles != 0;
         if ((B.cam_lists || B.bundles) && !list_stats) {
             list_stats = true;
