@@ -210,6 +210,16 @@ int yrt_scene_set_tile_lists(yrt_scene* ds, int mode);
  * entries, bundle lists} of the last render that built lists (a list that fell back to the
  * tree counts as its capacity + 1) */
 int yrt_scene_tile_lists(yrt_scene* ds, int* camera_on, int* bundles_on, unsigned long long* sums);
+/* LDS staging of the instance tree's hot top (the north_star's "hot node tiles staged in LDS";
+ * DESIGN.md §5). on = 1: yrt_render's persistent closest-hit grid copies the first 511
+ * camera-relative spine records, and its persistent any-hit grid the first 85 4-wide records
+ * (scenes with at least that many), into LDS once per block, and the walks read those records
+ * from LDS instead of through the scalar cache. The tile lists are not built while it is on:
+ * their walks start below the tree's top. Identical images either way. Off (0) by default:
+ * measured slower, the top records being scalar-cache hits already. Set it between renders. */
+int yrt_scene_set_lds_staging(yrt_scene* ds, int on);
+/* what the last yrt_render on this handle staged: bit 0 the closest hit, bit 1 the any hit */
+int yrt_scene_lds_staging(yrt_scene* ds, int* staged);
 /* counters of the last render/trace call on this handle (synchronises the stream) */
 int yrt_last_stats(yrt_scene* ds, yrt_stats* stats);
 /* per-phase GPU times of the last yrt_render with p->timing = 1 (synchronises) */

@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # knob -> the non-default defines compiled here
 VARIANTS = {
-    "YRT_SHADOW_LDS_RECORDS": ["-DYRT_SHADOW_LDS_RECORDS=85"],
+    "YRT_SHADOW_LDS_RECORDS": ["-DYRT_SHADOW_LDS_RECORDS=341"],
     "YRT_DEBUG_BOUNDS": ["-DYRT_DEBUG_BOUNDS"],
     "YRT_WIDE_STATS": ["-DYRT_WIDE_STATS"],
     "YRT_TAIL_STATS": ["-DYRT_TAIL_STATS"],
@@ -44,7 +44,7 @@ VARIANTS = {
     "YRT_BUNDLE_ITEMS": ["-DYRT_BUNDLE_ITEMS=16", "-DYRT_BUNDLE_MIN_TOP=0"],
     "YRT_SKIP_UNUSED_V": ["-DYRT_SKIP_UNUSED_V=0"],
     "YRT_SHADE_LEVEL_WAVES": ["-DYRT_SHADE_LEVEL_WAVES=7"],
-    "YRT_PRIMARY_LDS_RECORDS": ["-DYRT_PRIMARY_LDS_RECORDS=511"],
+    "YRT_PRIMARY_LDS_RECORDS": ["-DYRT_PRIMARY_LDS_RECORDS=1023"],
     "YRT_PRIMARY_WAVES": ["-DYRT_PRIMARY_WAVES=6", "-DYRT_PRIMARY_SP_BLOCK=768"],
     "YRT_FAST_NORMALIZE": ["-DYRT_FAST_NORMALIZE=0"],
     # round 5: the conservative inner-slot test of the any-hit walk (both forms lost)

@@ -62,13 +62,17 @@ def main():
     runs = []
     scene = str(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.yrtscene").encode()
     for spec in a.libs:
-        path, _, lists = spec.partition("@")  # lib.so@auto|on|off: yrt_scene_set_tile_lists
+        # lib.so@auto|on|off: yrt_scene_set_tile_lists; lib.so@lds: yrt_scene_set_lds_staging
+        path, _, lists = spec.partition("@")
         lib, N = bind(path)
         hs, ds = C.c_void_p(), C.c_void_p()
         assert lib.yrt_scene_load(scene, C.byref(hs)) == 0, lib.yrt_last_error()
         assert lib.yrt_host_scene_build_bvh(hs, 0) == 0
         assert lib.yrt_scene_upload(hs, 0, C.byref(ds)) == 0, lib.yrt_last_error()
-        if lists:
+        if lists == "lds":
+            lib.yrt_scene_set_lds_staging.argtypes = [C.c_void_p, C.c_int]
+            assert lib.yrt_scene_set_lds_staging(ds, 1) == 0
+        elif lists:
             lib.yrt_scene_set_tile_lists.argtypes = [C.c_void_p, C.c_int]
             assert lib.yrt_scene_set_tile_lists(ds, {"auto": 0, "on": 1, "off": 2}[lists]) == 0
         p = N.RenderParams()

@@ -194,6 +194,18 @@ class DeviceScene:
         return {"camera": bool(cam.value), "bundles": bool(bun.value), "camera_entries": int(sums[0]),
                 "camera_lists": int(sums[1]), "bundle_entries": int(sums[2]), "bundle_lists": int(sums[3])}
 
+    def set_lds_staging(self, on: bool) -> None:
+        """LDS staging of the instance tree's top in render_into's persistent walks (the tile
+        lists are not built while it is on; identical images; off by default, measured slower:
+        DESIGN.md §5)"""
+        check(N.lib.yrt_scene_set_lds_staging(self._h, 1 if on else 0), "set_lds_staging")
+
+    def lds_staging(self) -> dict:
+        """which walks of the last render read the staged records"""
+        v = C.c_int()
+        check(N.lib.yrt_scene_lds_staging(self._h, C.byref(v)), "lds_staging")
+        return {"closest_hit": bool(v.value & 1), "any_hit": bool(v.value & 2)}
+
     @property
     def device_bytes(self) -> int:
         return int(N.lib.yrt_scene_device_bytes(self._h))

@@ -120,6 +120,8 @@ _sig = {
     "yrt_scene_set_trace_algorithm": (C.c_int, [_vp, C.c_int]),
     "yrt_scene_set_tile_lists": (C.c_int, [_vp, C.c_int]),
     "yrt_scene_tile_lists": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_ulonglong)]),
+    "yrt_scene_set_lds_staging": (C.c_int, [_vp, C.c_int]),
+    "yrt_scene_lds_staging": (C.c_int, [_vp, C.POINTER(C.c_int)]),
     "yrt_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "yrt_last_timings": (C.c_int, [_vp, C.POINTER(Timings)]),
     "yrt_tonemap": (C.c_int, [_vp, C.c_int, _vp, C.c_int, _vp]),

@@ -421,6 +421,18 @@ int yrt_scene_tile_lists(yrt_scene* s, int* camera_on, int* bundles_on, unsigned
     });
 }
 
+int yrt_scene_set_lds_staging(yrt_scene* s, int on) {
+    if (!s || (on != 0 && on != 1)) return YRT_ERR_INVALID_ARG;
+    s->ds->lds_staging = on;
+    return YRT_OK;
+}
+
+int yrt_scene_lds_staging(yrt_scene* s, int* staged) {
+    if (!s || !staged) return YRT_ERR_INVALID_ARG;
+    *staged = s->ds->last_lds_staging;
+    return YRT_OK;
+}
+
 size_t yrt_scene_device_bytes(const yrt_scene* s) { return s && s->ds ? s->ds->arena_bytes : 0; }
 
 void yrt_scene_free(yrt_scene* s) {

@@ -808,9 +808,11 @@ constexpr int SP_BLOCK = 1024;  // threads per persistent block (two blocks per 
 #endif
 static_assert((YRT_PRIMARY_WAVES * 4 * 64) % YRT_PRIMARY_SP_BLOCK == 0, "whole blocks per CU");
 #ifndef YRT_PRIMARY_LDS_RECORDS
-// k_primary_persist: the first records of the camera-relative instance level (breadth first,
-// device_scene.cpp) staged in LDS per block, read by the walk instead of through the scalar cache
-#define YRT_PRIMARY_LDS_RECORDS 0
+// k_primary_persist with LDS staging on (yrt_scene_set_lds_staging): the first records of the
+// camera-relative instance level (breadth first, device_scene.cpp) staged in LDS per block and
+// read by the walk instead of through the scalar cache (A/B, DESIGN.md §5: 1 023 / 511 / 255
+// records +4.1 / +3.7 / +4.3 %; the handle's default is off)
+#define YRT_PRIMARY_LDS_RECORDS 511
 #endif
 #ifndef YRT_PRIMARY_PERSIST_MIN_ITEMS
 // A/B against k_primary (items = 64-sample blocks; profiles/r3/ab_primary_persist): 2.07 M
@@ -1578,7 +1580,9 @@ __global__ __launch_bounds__(256) void k_list_stats(wf_buffers B, int ntiles, in
 #define YRT_SHADOW_PERSIST_MIN_ITEMS 262144
 #endif
 #ifndef YRT_SHADOW_LDS_RECORDS
-#define YRT_SHADOW_LDS_RECORDS 0  // 4-wide records staged in LDS per block (persistent kernel only; A/B: 21 / 85 / 341 records +2 / +2 / +3 %)
+// k_shadow_persist with LDS staging on (yrt_scene_set_lds_staging): the 4-wide records staged
+// in LDS per block (A/B: 21 / 85 / 341 records +2 / +2 / +3 %; the handle's default is off)
+#define YRT_SHADOW_LDS_RECORDS 85
 #endif
 
 template <int LDSN>
@@ -2120,6 +2124,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         if (e != hipSuccess) return e;
     }
     phase_timer& T = ds.timer;
+    // LDS staging of the instance tree's top (yrt_scene_set_lds_staging): the persistent walks
+    // read it from LDS; the tile lists, whose walks start below it, are not built
+    const bool stage = ds.lds_staging != 0 && !COUNT && PACKET;
+    ds.last_lds_staging = 0;
     const float4 cam4 = make_float4(A.cam.ox, A.cam.oy, A.cam.oz, 0.0f);
     const int stride_grid = 2048;  // grid-stride kernels: 8 blocks of 256 per CU
     // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE;
@@ -2139,12 +2147,12 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         // any frame size when the caller forces the lists on (the bundles live there)
         const bool shadow_persist = !COUNT && PACKET && ds.wide_ok && TB == 64 && ds.nlights > 0 &&
                                     ((long long)tgrid * ds.nlights >= YRT_SHADOW_PERSIST_MIN_ITEMS ||
-                                     ds.lists_mode == 1);
+                                     ds.lists_mode == 1 || stage);
         // ... and walk the bundles' candidate lists (k_bundle_lists) instead of the tree
-        const bool bundles_possible = YRT_SHADOW_BUNDLES && YRT_SHADOW_LDS_RECORDS == 0 && shadow_persist &&
+        const bool bundles_possible = YRT_SHADOW_BUNDLES && !stage && shadow_persist &&
                                       bundle_lights(ds.nlights) > 0 && ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
         // the camera rays walk their tiles' leaf lists (k_camera_lists)
-        const bool cam_lists_possible = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !COUNT && PACKET && ds.wide_ok &&
+        const bool cam_lists_possible = YRT_CAMERA_LISTS && YRT_PRIMARY_REL && !stage && !COUNT && PACKET && ds.wide_ok &&
                                         ds.view.nwtop >= YRT_BUNDLE_MIN_TOP;
         // YRT_LISTS_ON: whenever the scene allows; YRT_LISTS_AUTO: the same from
         // YRT_LISTS_MIN_SPP samples per pixel; _OFF: never (yrt_scene_set_tile_lists)
@@ -2179,11 +2187,15 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 if (e != hipSuccess) return e;
                 const int nb = ds.num_cus * (YRT_PRIMARY_WAVES * 4 * 64 / YRT_PRIMARY_SP_BLOCK);
                 if (B.cam_lists)
-                    hipLaunchKernelGGL((k_primary_persist<SE, YRT_PRIMARY_LDS_RECORDS, true>), dim3(nb),
-                                       dim3(YRT_PRIMARY_SP_BLOCK), 0, stream, ds.view, A, C, B, counters);
-                else
+                    hipLaunchKernelGGL((k_primary_persist<SE, 0, true>), dim3(nb), dim3(YRT_PRIMARY_SP_BLOCK), 0,
+                                       stream, ds.view, A, C, B, counters);
+                else if (stage && YRT_PRIMARY_REL) {
                     hipLaunchKernelGGL((k_primary_persist<SE, YRT_PRIMARY_LDS_RECORDS, false>), dim3(nb),
                                        dim3(YRT_PRIMARY_SP_BLOCK), 0, stream, ds.view, A, C, B, counters);
+                    ds.last_lds_staging |= 1;
+                } else
+                    hipLaunchKernelGGL((k_primary_persist<SE, 0, false>), dim3(nb), dim3(YRT_PRIMARY_SP_BLOCK), 0,
+                                       stream, ds.view, A, C, B, counters);
             }
         }
         if (!persist) {
@@ -2238,10 +2250,11 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                         if (e != hipSuccess) return e;
                     }
                     constexpr int L = YRT_SHADOW_LDS_RECORDS;
-                    if (L > 0 && ds.view.nwtop >= L)
+                    if (stage && L > 0 && ds.view.nwtop >= L) {  // (the copy reads L whole records)
                         hipLaunchKernelGGL((k_shadow_persist<L>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
                                            nsamp, tgrid, B, counters, cam4);
-                    else
+                        ds.last_lds_staging |= 2;
+                    } else
                         hipLaunchKernelGGL((k_shadow_persist<0>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
                                            nsamp, tgrid, B, counters, cam4);
                 } else if (!COUNT && PACKET && ds.wide_ok)

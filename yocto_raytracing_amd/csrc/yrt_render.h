@@ -77,6 +77,9 @@ struct device_scene {
     // shadow rays on the persistent grid at any frame size); YRT_LISTS_OFF: never
     int lists_mode = 0;
     bool last_camera_lists = false, last_bundles = false;  // what the last render used
+    // yrt_scene_set_lds_staging: the persistent walks read the instance tree's top from LDS
+    int lds_staging = 0;
+    int last_lds_staging = 0;  // what the last render staged: bit 0 closest hit, bit 1 any hit
     phase_timer timer;
 };
 
