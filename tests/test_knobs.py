@@ -26,6 +26,7 @@ VARIANTS = {
     "YRT_SHADOW_LDS_RECORDS": ["-DYRT_SHADOW_LDS_RECORDS=341"],
     "YRT_DEBUG_BOUNDS": ["-DYRT_DEBUG_BOUNDS"],
     "YRT_WIDE_STATS": ["-DYRT_WIDE_STATS"],
+    "YRT_LIST_TIMING": ["-DYRT_LIST_TIMING"],
     "YRT_TAIL_STATS": ["-DYRT_TAIL_STATS"],
     "YRT_NT_STREAMS": ["-DYRT_NT_STREAMS=0"],
     "YRT_SHARED_TAIL": ["-DYRT_SHARED_TAIL=0"],

@@ -1143,6 +1143,23 @@ __device__ __forceinline__ bool light_position(const dev_scene_view& S, int li, 
     return ident && __builtin_isfinite(Lp.x) && __builtin_isfinite(Lp.y) && __builtin_isfinite(Lp.z);
 }
 
+#ifdef YRT_LIST_TIMING
+// diagnostic build only (tools/list_timing.py): per wave of the list builders, phase times
+// on the 100 MHz constant clock and a size (vector stores by lane 0)
+static __device__ unsigned long long g_list_time[3][65536][4];
+#define YRT_LT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define YRT_LT_WRITE(k, i, a, b, c, d)                                                          \
+    do {                                                                                        \
+        if (lane == 0 && (unsigned)(i) < 65536u) {                                              \
+            unsigned long long* e_ = g_list_time[k][i];                                         \
+            e_[0] = (a), e_[1] = (b), e_[2] = (c), e_[3] = (d);                                 \
+        }                                                                                       \
+    } while (0)
+#else
+#define YRT_LT_STAMP(v)
+#define YRT_LT_WRITE(k, i, a, b, c, d)
+#endif
+
 #ifndef YRT_BUNDLE_SUPER
 // two-level build: one tree walk per (super-bundle of 4 consecutive bundles, light) into a
 // list of up to super_max leaves, which each bundle then filters with its own planes
@@ -1163,6 +1180,7 @@ __global__ __launch_bounds__(256) void k_bundle_super(dev_scene_view S, wf_buffe
     const int nsuper = (n_items + super_bundles * bundle_g - 1) / (super_bundles * bundle_g);
     const int sl = blockIdx.x * 4 + w;
     if (sl >= nsuper * nl) return;  // (whole waves)
+    YRT_LT_STAMP(lt0);
     const int sg = sl / nl, li = sl - sg * nl;
     f4* out = B.slists + (size_t)sl * super_list_f4;
     float plx, ply, plz, phx, phy, phz;
@@ -1172,6 +1190,7 @@ __global__ __launch_bounds__(256) void k_bundle_super(dev_scene_view S, wf_buffe
     vec3f Lp;
     const bool lok = light_position(S, li, Lp);
     int nc = -1;
+    YRT_LT_STAMP(lt1);
     if (!ballot(bad) && lok) {
         if (!(plx <= phx)) {
             nc = 0;
@@ -1189,6 +1208,8 @@ __global__ __launch_bounds__(256) void k_bundle_super(dev_scene_view S, wf_buffe
             (lane & 1) ? float4{e[3], e[4], e[5], 0.0f} : float4{e[0], e[1], e[2], e[6]};
     }
     if (lane == 0) reinterpret_cast<float4*>(out)[0] = float4{__int_as_float(nc), 0.0f, 0.0f, 0.0f};
+    YRT_LT_STAMP(lt2);
+    YRT_LT_WRITE(1, sl, lt1 - lt0, lt2 - lt1, 0ull, (unsigned long long)(unsigned)nc);
 }
 
 // one wave per (bundle, light): the candidate list (see above) -- from the super-bundle's
@@ -1200,6 +1221,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
     const int ngroups = (n_items + bundle_g - 1) / bundle_g;
     const int gl = blockIdx.x * 4 + w;
     if (gl >= ngroups * nl) return;  // (whole waves)
+    YRT_LT_STAMP(lt0);
     const int g = gl / nl, li = gl - g * nl;
     float plx, ply, plz, phx, phy, phz;
     bool bad;
@@ -1253,6 +1275,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         return;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the candidate stores, before any lane reads them
+    YRT_LT_STAMP(lt1);
     if (YRT_BUNDLE_SORT && nc > 1) {
         // the leaves in the order the bundle's rays meet them (box centres projected on the
         // direction from the hit points to the light; YRT_BUNDLE_SORT), so that the chain's
@@ -1321,6 +1344,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         nc = __popcll(km);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    YRT_LT_STAMP(lt2);
     // the list as wide records at B.lists + gl * bundle_recs: up to 4 leaves in the root;
     // more in up to 4 child records of 4, the root's slot c holding child c's box (the union
     // of its leaves' boxes) and its byte offset from B.lists
@@ -1360,6 +1384,8 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         reinterpret_cast<float4*>(B.lists)[(size_t)(rec0 + rq) * 8 + row] = o;
     }
     if (lane == 0) B.lcount[gl] = nc;
+    YRT_LT_STAMP(lt3);
+    YRT_LT_WRITE(2, gl, lt1 - lt0, lt2 - lt1, lt3 - lt2, (unsigned long long)(unsigned)nc);
 }
 
 // ---- camera lists: per 8x8-pixel tile of the chunk, a frontier of the reference's instance
@@ -1388,6 +1414,7 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     const int ntiles = C.npix / (TILE * TILE);
     const int t = blockIdx.x * 4 + w;
     if (t >= ntiles) return;  // (whole waves)
+    YRT_LT_STAMP(lt0);
     const long long T = C.pix0 / (TILE * TILE) + t;
     const int lx0 = (int)(T % C.tiles_x) * TILE, ly0 = (int)(T / C.tiles_x) * TILE;
     // the tile's image columns and rows (bands interleave the rows: take their range)
@@ -1453,7 +1480,14 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
         nf = outside(rl, rh) ? 0 : 1;
         if (lane == 0) fr[w][0][0][0] = rl, fr[w][0][0][1] = rh;
     }
+#ifdef YRT_LIST_TIMING
+    int nrounds = 0;
+#endif
+    YRT_LT_STAMP(lt1);
     for (int round = 0; round < 64 && nf > 0; round++) {
+#ifdef YRT_LIST_TIMING
+        nrounds++;
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         float4 lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0}, alo = lo, ahi = lo, blo = lo, bhi = lo;
         bool inner = false, ka = false, kb = false;
@@ -1492,6 +1526,7 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
         cur ^= 1;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    YRT_LT_STAMP(lt2);
     float4 elo = {0, 0, 0, 0}, ehi = {0, 0, 0, 0};
     bool keep = false;
     if (lane < nf) {
@@ -1528,6 +1563,8 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     }
     nf = __popcll(km);
     if (lane == 0) B.ccount[t] = nf;
+    YRT_LT_STAMP(lt3);
+    YRT_LT_WRITE(0, t, lt1 - lt0, lt2 - lt1, lt3 - lt2, (unsigned long long)nrounds << 32 | (unsigned)nf);
 }
 
 // the sums of one chunk's list lengths into B.lstats (a list that fell back to the tree counts
@@ -2362,6 +2399,21 @@ extern "C" int yrt_debug_first_stats(unsigned long long* out16, int reset) {
     if (reset) {
         static const unsigned long long z[1024 * 16] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_first_stats), z, sizeof z);
+    }
+    return 0;
+}
+#endif
+
+#ifdef YRT_LIST_TIMING
+// out: n x {phase times..., size} of list builder k (0 k_camera_lists, 1 k_bundle_super,
+// 2 k_bundle_lists), n <= 65536; reset: zero them afterwards
+extern "C" int yrt_debug_list_time(unsigned long long* out, int k, int n, int reset) {
+    if (k < 0 || k > 2 || n < 0 || n > 65536) return -1;
+    const size_t off = (size_t)k * sizeof(yrt::g_list_time[0]);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(yrt::g_list_time), (size_t)n * 32, off) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long z[65536 * 4];
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(yrt::g_list_time), z, sizeof z, off);
     }
     return 0;
 }
