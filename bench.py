@@ -17,16 +17,25 @@ is fixed as N grows ("scaling": "strong").
 its own N ranks (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) before
 anything touches the GPU; rank 0 prints the one JSON line.
 
-value     all rays traced by all ranks (camera + shadow + reflection, the reference's
-          intersect_first + intersect_any calls) / wall time of K frames
-roofline  the dominant kernel (k_shadow at c4) is bound by instruction ISSUE, not by
-          HBM (its 2.9 MB scene is cache-resident): achieved = its scalar- or vector-
-          instruction count per launch (rocprofv3 SQ_INSTS_SALU / SQ_INSTS_VALU,
-          committed under profiles/, tools/gpu_issue_pmc.sh) / its mean launch time
-          measured live with HIP events on the launch stream, against the chip's issue
-          peak (one SALU per CU per clock; one wave64 VALU per SIMD per two clocks; 256
-          CUs at 2.4 GHz). The pipe with the higher fraction is the bound. The HBM
-          fraction from the FETCH_SIZE/WRITE_SIZE passes is reported beside it.
+value     the reference's ray count over all ranks (camera + shadow + reflection rays, its
+          intersect_first + intersect_any calls, src/raytrace.cpp:121-133) / wall time of K
+          frames. A shadow ray whose light term is exactly zero is counted there but answered
+          without a walk (the shadow cull); config.rays_traced_per_frame and
+          config.Mrays_traced_per_s give the rays actually walked, config.shadow_rays_culled_per_frame
+          the difference
+roofline  the roofline kernel is the longest per-ray phase of this run's frame (the
+          per-render lists phase, fixed work whatever a rank's share, is never picked;
+          roofline_phase()): the closest hit k_primary_persist at c4. The walks are bound by
+          instruction ISSUE, not by HBM (the 2.9 MB scene is cache-resident): achieved = the
+          kernel's scalar- or vector-instruction count per launch (rocprofv3 SQ_INSTS_SALU /
+          SQ_INSTS_VALU, committed under profiles/, tools/gpu/issue_pmc.sh) / its mean launch
+          time measured live with HIP events on the launch stream, against the chip's issue
+          peak (one SALU per CU per clock; one wave64 VALU per SIMD per two clocks; 256 CUs at
+          2.4 GHz). The pipe with the higher fraction is the bound. The HBM fraction from the
+          FETCH_SIZE/WRITE_SIZE passes is reported beside it; roofline_walks gives both walks'
+          (closest hit and any hit) issue rooflines
+frame     frame_sha256 of rank 0's reassembled frame, and frame_matches_n1 against the N = 1
+          digest committed for this workload (profiles/frame_digests.json)
 cpu_baseline  the reference itself (oracle/_ref, compiled from the unmodified sources)
           on a bounded sample of rows of the same frame, single thread, three disjoint
           row sets (value pooled, spread per set); cpu_baseline_all_cores the reference
@@ -59,10 +68,18 @@ N_CU, CLOCK_HZ = 256, 2.4e9
 SALU_PEAK = N_CU * 1.0 * CLOCK_HZ / 1e9   # G wave-instructions/s
 VALU_PEAK = N_CU * 4 * 0.5 * CLOCK_HZ / 1e9
 BAND = 8
-PHASE_KERNEL = {"primary": "k_primary<false, true, unsigned int>",
+# the kernel each phase's time is dominated by on the timed path (the lists-on c4 frame;
+# profiles/r*/final/pmc_c4/ks_kernel_stats.csv)
+PHASE_KERNEL = {"primary": "k_primary_persist<unsigned int, 0, true>",
                 "shadow": "k_shadow_persist<0>",
                 "shade": "k_shade<false, true, 256, true>",
+                "bounce": "k_bounce<false, true, unsigned int>",
                 "megakernel": "render_kernel<false>"}
+# phases whose work is fixed per render, not per ray (the camera-relative records and the
+# tile lists): never the roofline kernel -- at a small rank share their launch latency can
+# outlast a walk without saying anything about the walks
+FIXED_PHASES = ("lists",)
+DIGESTS = ROOT / "profiles" / "frame_digests.json"
 
 
 def parse():
@@ -80,7 +97,7 @@ def parse():
     p.add_argument("--algorithm", default="wavefront", choices=("wavefront", "megakernel", "wavefront_lane"))
     p.add_argument("--profile-rank", default="",
                    help="R/N: one process renders rank R's bands of an N-rank run, no gather (the counter "
-                        "passes for the N-rank roofline, tools/gpu_issue_pmc.sh); its line is not a bench result")
+                        "passes for the N-rank roofline, tools/gpu/issue_pmc.sh); its line is not a bench result")
     p.add_argument("--no-count-pass", action="store_true",
                    help="skip the untimed instrumented pass that gives SURVEY §8(d)'s algorithmic bytes")
     p.add_argument("--dry-run", action="store_true",
@@ -338,6 +355,30 @@ def issue_roofline(issue_json: Path, key: str, kernel_ms: float, identity: str, 
     return bound, pipes, rec
 
 
+def roofline_phase(phases: dict) -> str:
+    """the phase whose kernel the line's roofline describes: the longest of this frame's
+    per-ray phases ({phase: (ms, launches)}), never a fixed per-render phase (FIXED_PHASES)"""
+    per_ray = {k: v for k, v in phases.items() if k not in FIXED_PHASES and v[1] > 0}
+    pool = per_ray or phases
+    return max(pool, key=lambda k: pool[k][0])
+
+
+def digest_key(scene: str, W: int, H: int, samples: int) -> str:
+    return f"{scene}-{W}x{H}-s{samples}"
+
+
+def frame_matches_n1(digest, key: str, path: Path = DIGESTS):
+    """whether this frame's sha256 equals the committed N = 1 digest of the workload (None
+    when there is no digest to compare: no frame, or no committed entry)"""
+    if digest is None:
+        return None
+    try:
+        want = json.loads(Path(path).read_text()).get(key)
+    except (OSError, ValueError):
+        return None
+    return None if want is None else digest == want
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -451,7 +492,7 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ds.last_stats()
     phases = ds.last_timings()  # {phase: (ms over the K steps, launches)}
-    dom = max(phases, key=lambda k: phases[k][0])
+    dom = roofline_phase(phases)
     dom_ms = phases[dom][0] / a.steps  # per frame
     dom_launches = phases[dom][1] / a.steps
     render_ms = sum(v[0] for v in phases.values()) / a.steps
@@ -494,13 +535,14 @@ def main():
         params.count_work = 0
 
     t = torch.tensor([elapsed, dom_ms, render_ms, e2e_ms], dtype=torch.float64, device=dev)
-    rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps, algo_bytes], dtype=torch.float64,
-                        device=dev)
+    rays = torch.tensor([st["rays"] * a.steps, st["camera_samples"] * a.steps, algo_bytes,
+                         st["shadow_rays_culled"] * a.steps], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
     elapsed, dom_ms, render_ms, e2e_ms = (float(v) for v in t)
     total_rays, total_samples, total_algo_bytes = float(rays[0]), float(rays[1]), float(rays[2])
+    total_culled = float(rays[3])
 
     if rank == 0:
         spp = a.samples * a.samples
@@ -517,6 +559,19 @@ def main():
         key_n1 = f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-{dom}"
         share = (st["rays"] * a.steps) / total_rays if total_rays else 1.0  # rank 0's share of the frame
         bound, pipes, rec = issue_roofline(Path(a.issue_json), key, kernel_ms, identity, key_n1, share)
+        # both walks' issue rooflines (the closest hit and the any hit), whichever is longer
+        walks = {}
+        for ph in ("primary", "shadow"):
+            if ph not in phases or not phases[ph][1]:
+                continue
+            ph_ms = phases[ph][0] / phases[ph][1]
+            wb, wp, wr = issue_roofline(Path(a.issue_json), f"{a.scene}-{W}x{H}-s{a.samples}-n{band_world}-"
+                                        f"{a.algorithm}-{ph}", ph_ms, identity,
+                                        f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-{ph}", share)
+            walks[ph] = ({"kernel": wr.get("kernel", PHASE_KERNEL.get(ph, ph)), "kernel_ms": ph_ms, "bound": wb,
+                          "frac": wp[wb]["frac"], "salu_frac": wp["salu"]["frac"], "valu_frac": wp["valu"]["frac"]}
+                         if wb else {"kernel": PHASE_KERNEL.get(ph, ph), "kernel_ms": ph_ms, "frac": None,
+                                     "note": wr})
         if bound:
             roof = {"bound": "issue", "pipe": bound, "achieved": pipes[bound]["achieved"],
                     "peak": pipes[bound]["peak"], "unit": "G wave-instructions/s", "frac": pipes[bound]["frac"],
@@ -533,7 +588,7 @@ def main():
             roof = {"bound": "issue", "achieved": None, "peak": None, "unit": "G wave-instructions/s",
                     "frac": None, "traffic": traffic, "kernel": PHASE_KERNEL.get(dom, dom),
                     "kernel_ms": kernel_ms, "code_identity": identity,
-                    "note": f"{rec} (tools/gpu_issue_pmc.sh collects them)"}
+                    "note": f"{rec} (tools/gpu/issue_pmc.sh collects them)"}
         line = {
             "metric": metric,
             "value": total_rays / elapsed / 1e6,
@@ -553,6 +608,12 @@ def main():
                                        (" overlapped with the next frame" if overlap else "")) if world > 1
                        else "single GPU",
                        "rays_per_frame": total_rays / a.steps,
+                       "rays_traced_per_frame": (total_rays - total_culled) / a.steps,
+                       "shadow_rays_culled_per_frame": total_culled / a.steps,
+                       "Mrays_traced_per_s": (total_rays - total_culled) / elapsed / 1e6,
+                       "rays_note": ("value counts the reference's rays (intersect_first + intersect_any "
+                                     "calls); rays_traced_per_frame excludes the shadow rays whose light "
+                                     "term is exactly zero, answered without a walk (identical image)"),
                        "camera_samples_per_frame": total_samples / a.steps,
                        "gpu_ms_per_frame": render_ms,
                        "ms_per_frame_end_to_end": e2e_ms,
@@ -571,7 +632,9 @@ def main():
                          "reference's per-ray fetches of its AoS layout, not this path's traffic: the packet "
                          "walks fetch each record once per 64-ray wave from a cache-resident scene, so this "
                          "exceeds the HBM peak; roofline above is the bound that applies.")},
+            "roofline_walks": walks,
             "frame_sha256": frame_sha256,
+            "frame_matches_n1": frame_matches_n1(frame_sha256, digest_key(a.scene, W, H, a.samples)),
         }
         if a.profile_rank:  # a counter-collection run, not a bench result
             line["metric"] = f"profile of rank {a.profile_rank} (bands only, no gather): {metric}"

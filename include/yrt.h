@@ -84,13 +84,18 @@ typedef struct yrt_stats {
     unsigned long long texture_lookups;
     unsigned long long shadow_rays;     /* the shadow-ray phase alone (intersect_any calls; the
                                          * reference's count: a shadow ray whose light term is
-                                         * exactly zero is counted but not traced) */
+                                         * exactly zero is counted but not traced, DESIGN.md §5,
+                                         * see shadow_rays_culled) */
     unsigned long long shadow_box_tests;        /* count_work only */
     unsigned long long shadow_instance_entries; /* count_work only */
     unsigned long long shadow_prim_tests;       /* count_work only */
     unsigned long long wave_node_visits;        /* count_work, packet walk: node steps per wave */
     unsigned long long wave_prim_visits;        /* count_work, packet walk: primitive steps per wave */
     unsigned long long shadow_wave_node_visits; /* the same, shadow-ray phase alone */
+    unsigned long long shadow_rays_culled;      /* of shadow_rays: answered without a walk because
+                                                 * the light term is exactly zero (recorded as
+                                                 * occluded; 0 with count_work, which walks every
+                                                 * ray). Rays walked = rays - shadow_rays_culled */
 } yrt_stats;
 
 /* GPU time per kernel phase of the last render (HIP events on the launch stream) */

@@ -79,3 +79,30 @@ def test_code_identity_of_the_built_library():
     ident = mod.code_identity(lib)
     assert len(ident) == 64 and ident == mod.code_identity(lib)
     assert len(mod.code_objects(lib)) == 3  # render.hip, wavefront.hip, bvh_gpu.hip
+
+
+def test_roofline_phase_is_a_per_ray_phase():
+    """the roofline kernel of an N-rank line is the longest per-ray phase, never the per-render
+    lists phase: the one-GPU N = 2 rehearsal of round 5 (two ranks contending for one card)
+    timed lists at 76.7 ms and printed a roofline frac of 0.0007 for it"""
+    b = _bench_module()
+    rehearsal = {"primary": (9.1, 1), "shadow": (8.4, 1), "shade": (1.8, 1), "lists": (76.7, 4)}
+    assert b.roofline_phase(rehearsal) == "primary"
+    assert b.roofline_phase({"primary": (1.5, 1), "shadow": (1.6, 1), "lists": (0.1, 4)}) == "shadow"
+    # a phase with no launch is never picked; with nothing but fixed phases, the longest
+    assert b.roofline_phase({"primary": (0.0, 0), "megakernel": (3.0, 1), "lists": (9.0, 1)}) == "megakernel"
+    assert b.roofline_phase({"lists": (0.2, 2)}) == "lists"
+
+
+def test_frame_matches_n1(tmp_path):
+    b = _bench_module()
+    f = tmp_path / "digests.json"
+    key = b.digest_key("instance10000", 1920, 1080, 8)
+    assert key == "instance10000-1920x1080-s8"
+    f.write_text(json.dumps({key: "ab" * 32}))
+    assert b.frame_matches_n1("ab" * 32, key, f) is True
+    assert b.frame_matches_n1("cd" * 32, key, f) is False
+    assert b.frame_matches_n1("ab" * 32, "other-1x1-s1", f) is None
+    assert b.frame_matches_n1(None, key, f) is None
+    # the committed table holds the c4 digest of every round since round 2
+    assert b.frame_matches_n1("391c90ce91616fe38fd0fd2781a1c9f3d2ca41ebe9011a9f3740217f7760fc89", key) is True

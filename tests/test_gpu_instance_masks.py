@@ -32,7 +32,7 @@ def yrt():
     import yocto_raytracing_amd as y
 
     if not y.device_count():
-        pytest.skip("no GPU")
+        pytest.fail("no GPU visible: the -m gpu suite needs one")
     return y
 
 

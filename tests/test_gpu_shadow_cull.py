@@ -16,7 +16,11 @@ frame, and compare with the oracle (the reference's raytrace() through the C res
 
 Each frame is rendered with the tile lists forced on (the persistent any-hit grid: whole waves
 are culled) and off (the one-wave-block kernel: single lanes are culled); both must equal
-each other and the oracle."""
+each other and the oracle. The cull must leave the image bit for bit as tracing every ray does:
+the instrumented count_work pass walks every shadow ray (no cull), and its image must equal the
+default render's exactly, not just within the oracle tolerance. yrt_stats.shadow_rays_culled
+reports how many rays were answered without a walk: > 0 on these scenes, 0 on the count pass,
+and walked + culled = the reference's count."""
 from __future__ import annotations
 
 import numpy as np
@@ -32,7 +36,7 @@ def yrt():
     import yocto_raytracing_amd as y
 
     if not y.device_count():
-        pytest.skip("no GPU")
+        pytest.fail("no GPU visible: the -m gpu suite needs one")
     return y
 
 
@@ -98,9 +102,36 @@ def test_shadow_cull_equals_oracle(yrt, tmp_path, near_light):
     (on, st_on), (off, st_off) = out["on"], out["off"]
     np.testing.assert_array_equal(on.view(np.uint32), off.view(np.uint32))
     assert st_on == st_off
+    # culled rays exist here, and the count pass (every shadow ray walked) gives the same bits
+    assert 0 < st_on["shadow_rays_culled"] < st_on["shadow_rays"]
+    for mode in ("on", "off"):
+        ds.set_tile_lists(mode)
+        walked, st_w = yrt.raytrace(ds, (0.1, 0.1, 0.1), res, spp, return_stats=True, count_work=True)
+        np.testing.assert_array_equal(walked.view(np.uint32), on.view(np.uint32))
+        assert st_w["shadow_rays_culled"] == 0 and st_w["rays"] == st_on["rays"]
+        assert st_w["shadow_rays"] == st_on["shadow_rays"]
     ref, n, trunc = Oracle(str(path)).render(res, spp)
     assert trunc == 0 and n == st_on["rays"]  # culled rays are counted: the reference's count
+    walked_rays = st_on["rays"] - st_on["shadow_rays_culled"]
+    assert walked_rays + st_on["shadow_rays_culled"] == n and walked_rays < n
     differ = int(np.sum(on.view(np.uint32) != ref.view(np.uint32)))
     print(f"near_light={near_light}: {differ} of {on.size} channels not bit-exact vs oracle")
     assert close_mask(on, ref).all()
     assert np.mean(on.view(np.uint32) == ref.view(np.uint32)) > 0.99
+
+
+def test_shadow_cull_counts_at_c4_scale(yrt):
+    """instance10000 at 1080p, 1 spp (the c4 frame's geometry): culled rays are reported, the
+    count pass walks every one of them, and both images are the same bits"""
+    scn = yrt.load_scene(str(__import__("helpers").scene_path("instance10000")))
+    yrt.build_bvh(scn)
+    ds = scn.upload(0)
+    img, st = yrt.raytrace(ds, (0.1, 0.1, 0.1), 1080, 1, return_stats=True)
+    walked, st_w = yrt.raytrace(ds, (0.1, 0.1, 0.1), 1080, 1, return_stats=True, count_work=True)
+    np.testing.assert_array_equal(walked.view(np.uint32), img.view(np.uint32))
+    assert st["rays"] == st_w["rays"] == 4 * st["camera_samples"]  # the reference's 4.000 per sample
+    assert st_w["shadow_rays_culled"] == 0
+    frac = st["shadow_rays_culled"] / st["shadow_rays"]
+    print(f"instance10000 1080p 1 spp: {st['shadow_rays_culled']} of {st['shadow_rays']} shadow rays culled "
+          f"({frac:.3f})")
+    assert 0.0 < frac < 1.0

@@ -67,7 +67,7 @@ class Stats(C.Structure):
         "rays", "camera_samples", "depth_truncated", "stack_overflow", "box_tests",
         "instance_entries", "prim_tests", "shaded_hits", "texture_lookups", "shadow_rays",
         "shadow_box_tests", "shadow_instance_entries", "shadow_prim_tests", "wave_node_visits",
-        "wave_prim_visits", "shadow_wave_node_visits")]
+        "wave_prim_visits", "shadow_wave_node_visits", "shadow_rays_culled")]
 
 
 PHASES = ("primary", "shadow", "shade", "bounce", "fold", "accumulate", "megakernel", "lists")

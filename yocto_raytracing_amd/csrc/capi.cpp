@@ -589,6 +589,7 @@ int yrt_last_stats(yrt_scene* s, yrt_stats* out) {
         out->wave_node_visits = c[yrt::cnt_wave_node_visits];
         out->wave_prim_visits = c[yrt::cnt_wave_prim_visits];
         out->shadow_wave_node_visits = c[yrt::cnt_shadow_wave_node_visits];
+        out->shadow_rays_culled = c[yrt::cnt_shadow_culled];
         return YRT_OK;
     });
 }

@@ -93,8 +93,10 @@ int main(int argc, char** argv) {
         if (timing) {
             const yrt_stats st = yrt_cpp::last_stats(scn);
             double s = std::chrono::duration<double>(t1 - t0).count();
-            printf("render %dx%d x %d spp on %d GPU(s): %.3f ms (incl. copy to host), %llu rays, %.1f Mrays/s\n",
-                   hdr.width, hdr.height, samples * samples, gpus, s * 1e3, st.rays, st.rays / s / 1e6);
+            printf("render %dx%d x %d spp on %d GPU(s): %.3f ms (incl. copy to host), %llu rays, %.1f Mrays/s "
+                   "(%llu shadow rays with a zero light term answered without a walk)\n",
+                   hdr.width, hdr.height, samples * samples, gpus, s * 1e3, st.rays, st.rays / s / 1e6,
+                   st.shadow_rays_culled);
         }
         printf("saving image %s\n", out.c_str());
         yrt_cpp::save_hdr_or_ldr(out, hdr);

@@ -944,7 +944,7 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     const frame3f lf = {xyz(ld4(lr)), xyz(ld4(lr + 1)), xyz(ld4(lr + 2)), xyz(ld4(lr + 3))};
     const vec3f lp0 = xyz(ld4(lr + 4)), ke = xyz(ld4(lr + 5));
     work_counts wc;
-    unsigned long long rays = 0;
+    unsigned long long rays = 0, culled = 0;  // culled: counted in rays, answered without a walk
     const int stride = gridDim.x * BS;
     for (int g = 0; g < (level ? level_segments : 1); g++) {
     const int n = level ? *seg_counter(B.count, level, g) : nsamp_level0;
@@ -979,6 +979,7 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
             if (light_term_zero(info, xyz(s1), sr.o, xyz(ro4), sr.d, r, ke)) {
                 stb(B.occl + (size_t)li * B.capacity + idx, 1);
                 valid = false;
+                culled++;
             }
         }
         hit_record hr;
@@ -991,7 +992,7 @@ __global__ __launch_bounds__(shadow_block<PACKET>(), YRT_SHADOW_WAVES) void k_sh
     }
     }
     // shadow rays are counted once, here; yrt_last_stats reports rays = cnt_rays + this
-    flush_block<1, BS>(counters, {cnt_shadow_rays}, {rays});
+    flush_block<2, BS>(counters, {cnt_shadow_rays, cnt_shadow_culled}, {rays, culled});
     if (COUNT) {
         flush_work(counters, wc);
         flush(counters, cnt_shadow_box_tests, wc.box);
@@ -1641,7 +1642,9 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     const unsigned n_items = (unsigned)nx * (unsigned)nl;
     const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
-    unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays traced by this wave
+    unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays of this wave (the reference's count)
+    // per lane (a VGPR: one more SGPR would spill): this lane's rays answered without a walk
+    unsigned culled_l = 0;
     // positions from the block's chunk ring (chunk_ring_next), YRT_SHADOW_BLOCK_CHUNK at a time
     constexpr unsigned CS = YRT_SHADOW_BLOCK_CHUNK;
     __shared__ chunk_ring ring;
@@ -1685,14 +1688,15 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
             }
         }
         rays += (unsigned)__popcll(ballot(valid));
-        // the rays whose light term is zero (light_term_zero, in uniform control flow: its loads
-        // and ballots on every lane) start the walk as done -- recorded as occluded -- and a
-        // wave whose every ray is culled skips it. (Taking them out of `valid` instead trips the
-        // compiler inside this loop: "illegal VGPR to SGPR copy".)
-        const unsigned long long culled =
-            (YRT_SHADOW_CULL && !YRT_HIT16) ? ballot(valid && light_term_zero(info, xyz(s1), sr.o, cam_o, sr.d, r,
-                                                                                xyz(lrec[5])))
-                                             : 0ull;
+        // the rays whose light term is zero (light_term_zero, called by every lane in uniform
+        // control flow: its loads and ballots see the whole wave; it is false on a lane that is
+        // not a hit, info < 0, so it implies valid) start the walk as done -- recorded as
+        // occluded -- and a wave whose every ray is culled skips it. (Taking them out of `valid`
+        // instead trips the compiler inside this loop: "illegal VGPR to SGPR copy".)
+        const bool zero_term =
+            YRT_SHADOW_CULL && !YRT_HIT16 && light_term_zero(info, xyz(s1), sr.o, cam_o, sr.d, r, xyz(lrec[5]));
+        const unsigned long long culled = ballot(zero_term);
+        culled_l += zero_term ? 1u : 0u;
         const bool all_culled = YRT_SHADOW_CULL && !YRT_HIT16 && culled == ballot(valid);
         bool occ;
         int lc = -1;  // the bundle's list: its leaf count, -1 = walk the tree
@@ -1717,7 +1721,7 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
     tail_record(1, tail_t0, tail_items);
 #endif
     const unsigned long long mine = lane == 0 ? (unsigned long long)rays : 0ull;
-    flush_block<1, SP_BLOCK>(counters, {cnt_shadow_rays}, {mine});
+    flush_block<2, SP_BLOCK>(counters, {cnt_shadow_rays, cnt_shadow_culled}, {mine, (unsigned long long)culled_l});
 }
 
 // ---- shade() after the queries (raytrace.cpp:99-206) ----

@@ -171,14 +171,17 @@ enum counter_index {
     cnt_wave_node_visits = 13,
     cnt_wave_prim_visits = 14,
     cnt_shadow_wave_node_visits = 15,
-    cnt_count = 16
+    // shadow rays counted (the reference's intersect_any calls) but answered without a walk:
+    // their light term is exactly zero (wavefront.hip light_term_zero), recorded as occluded
+    cnt_shadow_culled = 16,
+    cnt_count = 32  // (17 used; a line is two 128-byte cache lines)
 };
 
-// The counters live in cnt_slots lines of cnt_count u64 (128 bytes each); a wave adds
+// The counters live in cnt_slots lines of cnt_count u64 (256 bytes each); a wave adds
 // its sums into the line picked by its global wave index and the host adds the lines.
 // One shared address for every wave serialises the device-scope atomics: with a
 // single line the per-wave counter flush alone cost ~30 ms of a 78 ms c4 shadow pass.
 constexpr int cnt_slots = 1024;
-static_assert(cnt_count * 8 == 128, "one counter line = one 128-byte cache line");
+static_assert(cnt_count * 8 % 128 == 0, "a counter line is whole 128-byte cache lines");
 
 }  // namespace yrt
