@@ -27,7 +27,7 @@ TIMED = {
     "k_shadow_persist<0> (c4 any hit)": (r"k_shadow_persistILi0EE", 0, 0, 27),
     "k_shade<fused, occ4> (c4 shading + per-pixel sum)": (r"k_shadeILb0ELb1ELi256ELb1EE", 0, 0, 16),
     "k_shade<level, occ4> (c3 mirror levels)": (r"k_shadeILb0ELb0ELi256ELb1EE", 0, 0, 52),
-    "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 37),
+    "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 39),
     "k_camera_lists": (r"k_camera_lists", 0, 0, 0),
     # (the list builders' 28 private bytes: a 7-float slot record indexed per lane, not spills)
     "k_bundle_lists": (r"k_bundle_lists", 0, 28, 0),

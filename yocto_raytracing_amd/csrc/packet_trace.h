@@ -451,10 +451,31 @@ __device__ __forceinline__ int wave_octant(vec3f invd, unsigned long long lanes)
     return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
 }
 
+#ifndef YRT_POP_ONE_EXIT
+#define YRT_POP_ONE_EXIT 1
+#endif
 // pop inside a descent: entries above `floor` until one with live lanes (true), or down
 // to the floor (false, mask 0) -- the level boundary is the caller's
 __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, int& node, unsigned long long& mask,
                                           int& sp, int stk_node, int stk_mlo, int stk_mhi) {
+#if YRT_POP_ONE_EXIT
+    // one exit block: the loop leaves through the same edge whether it found live lanes or
+    // reached the floor, and the empty asm hides m from the optimiser so that it cannot thread
+    // the caller's test back into the loop (two exit blocks make the structurizer's
+    // loop-exit unification route every descent step through a state variable)
+    unsigned long long m = 0;
+    while (sp > floor) {
+        sp--;
+        node = __builtin_amdgcn_readlane(stk_node, sp);
+        m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
+             (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
+            ~done;
+        if (m) break;
+    }
+    asm volatile("" : "+s"(m));
+    mask = m;
+    return m != 0;
+#else
     while (sp > floor) {
         sp--;
         node = __builtin_amdgcn_readlane(stk_node, sp);
@@ -465,6 +486,7 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
     }
     mask = 0;
     return false;
+#endif
 }
 
 constexpr int packet_block = 256;
@@ -491,6 +513,14 @@ constexpr int packet_block = 256;
 // LDSN > 0 (REL only): the first LDSN records of pbase are also in `lds` (staged per block by
 // k_primary_persist, YRT_PRIMARY_LDS_RECORDS); a record below that offset is read with
 // ds_read_b128 at a wave-uniform address instead of through the scalar cache
+#ifndef YRT_DESCENT_ONE_EXIT
+#define YRT_DESCENT_ONE_EXIT 1
+#endif
+#if YRT_DESCENT_ONE_EXIT
+#define YRT_DESCENT_EXIT break
+#else
+#define YRT_DESCENT_EXIT return
+#endif
 template <int OCT, bool COUNT, bool REL = false, int LDSN = 0>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
@@ -525,13 +555,13 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         mask = pm0;
         if (!pm0) {
             if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
-            return;
+            YRT_DESCENT_EXIT;
         }
         const int s0 = uniform(ibits(rec[0].w));
         const uint32_t c0 = (uint32_t)uniform(ibits(rec[1].w));
         if (c0 & leaf_bit) {
             node = s0, cl = c0;
-            return;
+            YRT_DESCENT_EXIT;
         }
         // push L (X's child start) for the lanes that passed X
         stk_node = writelane(stk_node, s0, sp);
@@ -543,13 +573,13 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         mask = pm1;
         if (!pm1) {
             if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
-            return;
+            YRT_DESCENT_EXIT;
         }
         const int s1 = uniform(ibits(rec[2].w));
         const uint32_t c1 = (uint32_t)uniform(ibits(rec[3].w));
         if (c1 & leaf_bit) {
             node = s1, cl = c1;
-            return;
+            YRT_DESCENT_EXIT;
         }
         // push RL (R's child start)
         stk_node = writelane(stk_node, s1, sp);
@@ -558,7 +588,14 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         sp++;
         node = s1 + spine_record_bytes;
     }
+#if YRT_DESCENT_ONE_EXIT
+    // every exit of the loop above arrives here; the empty asm makes the exit state opaque so
+    // that the caller's tests on it (leaf reached or not) are not threaded back into the loop
+    // as separate exit blocks
+    asm volatile("" : "+s"(mask), "+s"(node), "+s"(cl));
+#endif
 }
+#undef YRT_DESCENT_EXIT
 
 // ---- closest hit, laid out for the scalar unit ----
 // The packet discipline of packet_any (same node tests, in the reference's order, with
