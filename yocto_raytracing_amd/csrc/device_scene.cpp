@@ -509,6 +509,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     // (YRT_PRIMARY_LDS_RECORDS). Only the record numbering changes; the tree, and so the
     // walk's order of tests, is the reference's.
     std::vector<f4> tpair;
+    std::vector<int> tcut;
     {
         const size_t nn = tnodes.size() / 2;
         std::vector<uint32_t> bfs(nn, 0), order;  // old index -> breadth-first index, and back
@@ -535,6 +536,25 @@ device_scene* device_scene_create(const scene& scn, int device) {
             renum[2 * n] = lo, renum[2 * n + 1] = hi;
         }
         tpair = pairs(renum, 0, nn, 0);
+        // the camera lists' starting frontier (wavefront.hip k_camera_lists): the nodes of the
+        // tree's top cut_depth levels' cut -- every node at depth cut_depth, and every leaf above
+        // it -- in the reference's DFS order (child start+1 before start, scene.cpp:446-479), as
+        // byte offsets of their records in trel; at most 2^cut_depth entries
+        std::vector<std::pair<uint32_t, int>> st;  // (node, depth)
+        if (nn) st.push_back({0u, 0});
+        while (!st.empty()) {
+            const auto [n, d] = st.back();
+            st.pop_back();
+            uint32_t cl, start;
+            memcpy(&cl, &renum[2 * n + 1].w, 4);
+            memcpy(&start, &renum[2 * n].w, 4);
+            if ((cl & leaf_bit) || d == camera_cut_depth) {
+                tcut.push_back((int)(n * (uint32_t)spine_record_bytes));
+                continue;
+            }
+            st.push_back({start, d + 1});      // visited second
+            st.push_back({start + 1, d + 1});  // visited first, as the reference does
+        }
     }
     std::vector<f4> spair;
     for (size_t si = 0; si < scn.shapes.size(); si++) {
@@ -757,6 +777,7 @@ device_scene* device_scene_create(const scene& scn, int device) {
     size_t o_spair = ab.add(spair.data(), spair.size() * sizeof(f4));
     size_t o_tinst_id = ab.add(tinst_id.data(), tinst_id.size() * sizeof(int));
     size_t o_ibox = ab.add(ibox.data(), ibox.size() * sizeof(f4));
+    size_t o_tcut = ab.add(tcut.data(), tcut.size() * sizeof(int));
 
     try {
         check(hipSetDevice(device), "hipSetDevice");
@@ -802,6 +823,8 @@ device_scene* device_scene_create(const scene& scn, int device) {
     v.spair = (const f4*)(base + o_spair);
     v.tinst_id = (const int*)(base + o_tinst_id);
     v.ibox = ibox.empty() ? nullptr : (const f4*)(base + o_ibox);
+    v.tcut = (const int*)(base + o_tcut);
+    v.ntcut = (int)tcut.size();
     v.inst_masks = !ibox.empty() && tinst.size() / 4 < ((size_t)1 << 21) ? 1 : 0;
     v.wtop_root = wtop_root * wide_record_bytes;
     v.nwtop = wtop_records;

@@ -367,6 +367,10 @@ __device__ __attribute__((noinline)) float pow_f64_path(float x, float y) {
 }
 __device__ __forceinline__ float powf_cr(float x, float y) {
     if (y == 0.0f) return 1.0f;
+#ifdef YRT_DIAG_POW_F32
+    // diagnostic build only (an A/B of what the f64 path costs): NOT the reference's values
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+#endif
     // results below 2^-150 round to +0 (the f64 path gives exp2(-inf) = +0 for x = 0).
     // y * log2(x) < -151 by v_log_f32 (error ~2^-23 relative) puts the exact value below
     // -150 with a wide margin.

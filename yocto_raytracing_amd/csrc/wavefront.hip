@@ -1475,11 +1475,27 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     };
     const f4* trel = B.trel;
     const unsigned long long below = (1ull << lane) - 1ull;
+    // the frontier starts as the tree's top cut (S.tcut: the nodes at depth camera_cut_depth
+    // and the leaves above it, in DFS order) less the nodes the cone excludes -- one round of
+    // parallel loads instead of camera_cut_depth dependent ones from the root. A node whose
+    // ancestor the cone excludes is excluded too (its box lies inside the ancestor's), and an
+    // entry kept needlessly only costs its box test in the walk: the list stays exact.
+    static_assert((1 << camera_cut_depth) <= K, "the top cut fits one list");
     int nf, cur = 0;
     {
-        const float4 rl = ld4(trel), rh = ld4(trel + 1);
-        nf = outside(rl, rh) ? 0 : 1;
-        if (lane == 0) fr[w][0][0][0] = rl, fr[w][0][0][1] = rh;
+        float4 rl = {0, 0, 0, 0}, rh = {0, 0, 0, 0};
+        bool in = false;
+        if (lane < S.ntcut) {
+            const f4* r = trel + (size_t)((unsigned)S.tcut[lane] / 16u);
+            rl = ld4(r), rh = ld4(r + 1);
+            in = !outside(rl, rh);
+        }
+        const unsigned long long km0 = ballot(in);
+        if (in) {
+            const int q = __popcll(km0 & below);
+            fr[w][0][q][0] = rl, fr[w][0][q][1] = rh;
+        }
+        nf = __popcll(km0);
     }
 #ifdef YRT_LIST_TIMING
     int nrounds = 0;

@@ -82,6 +82,12 @@ constexpr int bundle_skip_shift = 21;
 constexpr uint32_t bundle_leaf_word(int first, int count, uint32_t skip) {
     return wide_leaf | (uint32_t)count << wide_count_shift | (skip & 0x7fu) << bundle_skip_shift | (uint32_t)first;
 }
+// the depth of the instance tree's cut the camera lists start from (k_camera_lists): 0 = the
+// root alone; at most 2^depth entries, which must fit one list (camera_list_max)
+#ifndef YRT_CAMERA_CUT_DEPTH
+#define YRT_CAMERA_CUT_DEPTH 5
+#endif
+constexpr int camera_cut_depth = YRT_CAMERA_CUT_DEPTH;
 constexpr int spine_len = 2;  // nodes per closest-hit walk record (a node and its child start+1)
 // spine records (tpair/spair): spine_len x {lo, hi} f4 pairs; an inner node's lo.w is
 // the byte offset of its child start's record (child start+1's is the next record)
@@ -115,6 +121,10 @@ struct dev_scene_view {
     // instance transforms (device_scene.cpp), NaN for frames it cannot bound; the list
     // builders drop the instances of a listed leaf that their cone or hull excludes
     const f4* ibox;
+    // the camera lists' starting frontier: the instance tree's cut at depth camera_cut_depth
+    // in the reference's DFS order, as byte offsets of the nodes' records (device_scene.cpp)
+    const int* tcut;
+    int ntcut;
     int inst_masks;  // 1: instance slots fit the bundle records' 21-bit first-slot field
     int wtop_root;
     int nwtop;  // records of the instance-level wide tree (breadth first: the top levels lead)
