@@ -41,7 +41,7 @@ VARIANTS = {
     "YRT_HIT16": ["-DYRT_HIT16=1"],
     "YRT_SHADOW_BUNDLES": ["-DYRT_SHADOW_BUNDLES=0"],
     "YRT_CAMERA_LISTS": ["-DYRT_CAMERA_LISTS=0"],
-    "YRT_CAMERA_LIST_MAX": ["-DYRT_CAMERA_LIST_MAX=12"],
+    "YRT_CAMERA_LIST_MAX": ["-DYRT_CAMERA_LIST_MAX=12", "-DYRT_CAMERA_CUT_DEPTH=3"],
     "YRT_BUNDLE_ITEMS": ["-DYRT_BUNDLE_ITEMS=16", "-DYRT_BUNDLE_MIN_TOP=0"],
     "YRT_SKIP_UNUSED_V": ["-DYRT_SKIP_UNUSED_V=0"],
     "YRT_SHADE_LEVEL_WAVES": ["-DYRT_SHADE_LEVEL_WAVES=7"],
@@ -54,6 +54,12 @@ VARIANTS = {
     "YRT_SHADOW_CULL": ["-DYRT_SHADOW_CULL=0"],
     "YRT_INSTANCE_MASKS": ["-DYRT_INSTANCE_MASKS=0"],
     "YRT_LISTS_MIN_SPP": ["-DYRT_LISTS_MIN_SPP=1"],
+    # round 6: the closest hit's one-exit descent and pop, the camera lists' top cut, the fused
+    # bundle lists, and the diagnostic (inexact) f32 pow of the f64-path A/B
+    "YRT_DESCENT_ONE_EXIT": ["-DYRT_DESCENT_ONE_EXIT=0", "-DYRT_POP_ONE_EXIT=0"],
+    "YRT_CAMERA_CUT_DEPTH": ["-DYRT_CAMERA_CUT_DEPTH=0"],
+    "YRT_BUNDLE_FUSED": ["-DYRT_BUNDLE_FUSED=1"],
+    "YRT_DIAG_POW_F32": ["-DYRT_DIAG_POW_F32"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change
     "YRT_R5_LANE": ["-DYRT_R5_LANE=0", "-DYRT_R5_UORIG=0", "-DYRT_R5_VCONST=0", "-DYRT_R5_IDXLANE=0", "-DYRT_R5_SURF=0"],
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],
@@ -63,7 +69,7 @@ VARIANTS = {
                           "-DYRT_PRIMARY_BLOCK_CHUNK=64"],
 }
 # knobs covered by another entry's defines
-COVERED = {"YRT_R5_UORIG", "YRT_R5_VCONST", "YRT_R5_IDXLANE", "YRT_R5_SURF", "YRT_BUNDLE_MIN_TOP", "YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
+COVERED = {"YRT_POP_ONE_EXIT", "YRT_R5_UORIG", "YRT_R5_VCONST", "YRT_R5_IDXLANE", "YRT_R5_SURF", "YRT_BUNDLE_MIN_TOP", "YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
            "YRT_SHADOW_PERSIST_MIN_ITEMS", "YRT_PRIMARY_PERSIST_MIN_ITEMS", "YRT_PRIMARY_BLOCK_CHUNK"}
 
 

@@ -489,7 +489,10 @@ int yrt_render(yrt_scene* s, const yrt_render_params* p, float* out, int mem, vo
         if (a.out_stride < r.tw) throw std::invalid_argument("out_stride smaller than the window width");
         size_t bytes = (size_t)a.out_stride * r.th * 4 * sizeof(float);
         void* dst = mem == YRT_MEM_DEVICE ? (void*)out : scratch(s, bytes);
-        hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long), st), "hipMemsetAsync");
+        // (the wavefront algorithms zero the counter lines in their first kernel, k_chunk_setup)
+        if (p->algorithm == YRT_ALGO_MEGAKERNEL)
+            hip_check(hipMemsetAsync(s->counters, 0, yrt::cnt_slots * yrt::cnt_count * sizeof(unsigned long long), st),
+                      "hipMemsetAsync");
         // timing 1: start a new record; 2: keep accumulating across calls (bench loops)
         if (!(p->timing == 2 && s->ds->timer.on)) s->ds->timer.reset(p->timing != 0);
         if (p->algorithm == YRT_ALGO_MEGAKERNEL && s->ds->reflective && a.max_depth > yrt::megakernel_max_depth)

@@ -472,6 +472,7 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
             ~done;
         if (m) break;
     }
+    m = (unsigned long long)(uint32_t)uniform((int)(m >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)m);
     asm volatile("" : "+s"(m));
     mask = m;
     return m != 0;
@@ -592,6 +593,12 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
     // every exit of the loop above arrives here; the empty asm makes the exit state opaque so
     // that the caller's tests on it (leaf reached or not) are not threaded back into the loop
     // as separate exit blocks
+    // (readfirstlane first: folded away where the compiler knows the values are in SGPRs, and
+    // the "s" constraints need them there where its uniformity analysis lost track, as in the
+    // YRT_DEBUG_BOUNDS build)
+    mask = (unsigned long long)(uint32_t)uniform((int)(mask >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)mask);
+    node = uniform(node);
+    cl = (uint32_t)uniform((int)cl);
     asm volatile("" : "+s"(mask), "+s"(node), "+s"(cl));
 #endif
 }

@@ -647,15 +647,32 @@ __device__ __forceinline__ bool primary_samples(const dev_scene_view& S, const d
     return valid;
 }
 
-// the instance-level spine records with the camera origin subtracted from every bound, in
-// fp32 as the reference's slab test does it ((bbox.min - ray.o), scene.cpp:373-374): what
-// the primary rays' REL walk reads (packet_first)
-__global__ __launch_bounds__(WF_BLOCK) void k_relative_records(const f4* __restrict__ rec, int n, float ox, float oy,
-                                                              float oz, f4* __restrict__ out) {
+// The instance-level spine records with the camera origin subtracted from every bound, in
+// fp32 as the reference's slab test does it ((bbox.min - ray.o), scene.cpp:373-374), are what
+// the primary rays' REL walk reads (packet_first); k_chunk_setup writes them once per render.
+
+// ---- per-chunk setup: one launch instead of a kernel and three to five fills ----
+// the camera-relative spine records (the first chunk of a packet render: tpair != nullptr),
+// and zeros for the persistent grids' work counters (queue), the list sums (lstats, the first
+// chunk that builds lists), the mirror levels' ray counts (count_ints) and the render's counter
+// lines (counters, the first chunk). Each fill was its own hipMemsetAsync launch of ~4 us of
+// GPU time; at a rank's share of an 8-way split a frame is ~2.6 ms.
+__global__ __launch_bounds__(WF_BLOCK) void k_chunk_setup(const f4* __restrict__ tpair, int nrec, float ox, float oy,
+                                                          float oz, f4* __restrict__ trel, unsigned* queue,
+                                                          unsigned long long* lstats, int* count, int count_ints,
+                                                          unsigned long long* counters, int counter_words) {
     const int i = blockIdx.x * WF_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const float4 r = ld4(rec + i);
-    out[i] = {r.x - ox, r.y - oy, r.z - oz, r.w};
+    const int stride = gridDim.x * WF_BLOCK;
+    if (tpair)
+        for (int k = i; k < nrec; k += stride) {
+            const float4 r = ld4(tpair + k);
+            trel[k] = {r.x - ox, r.y - oy, r.z - oz, r.w};
+        }
+    if (i < 32) queue[i] = 0u;
+    if (lstats && i < 4) lstats[i] = 0ull;
+    for (int k = i; k < count_ints; k += stride) count[k] = 0;
+    if (counters)
+        for (int k = i; k < counter_words; k += stride) counters[k] = 0ull;
 }
 
 // ---- work distribution of the persistent any-hit grid: block chunks ----
@@ -1063,14 +1080,17 @@ __device__ __forceinline__ bool hull_sep(const hull_t& H, float clx, float cly, 
 // the instance-level leaves the hull does not exclude, from a walk of the any-hit tree (lane
 // 16 s + j tests slot s of the current wide record against plane j; a lane-indexed stack):
 // up to CAP of them into cand (lane 0 writes), else overflow
+// only_slot >= 0: of the root record, only that slot's subtree (k_bundle_lists<FUSED> splits a
+// super-bundle's walk over a block's four waves by root slot)
 template <int CAP>
 __device__ __forceinline__ void hull_walk(const dev_scene_view& S, const hull_t& H, int lane, float (*cand)[8], int& nc,
-                                          bool& overflow) {
+                                          bool& overflow, int only_slot = -1) {
     const int s = lane >> 4;  // the slot this lane tests
     const f4* wbase = sgpr_ptr(S.wnodes);
     int stk = 0, sp = 0;
     nc = 0, overflow = false;
     uint32_t cur = (uint32_t)S.wtop_root;
+    bool root = true;
     for (;;) {
         float4 r[7];
         ld_wide_record(wbase, cur, r);
@@ -1084,6 +1104,8 @@ __device__ __forceinline__ void hull_walk(const dev_scene_view& S, const hull_t&
             const uint32_t wq = ubits(q == 0 ? r[6].x : q == 1 ? r[6].y : q == 2 ? r[6].z : r[6].w);
             if (wq != wide_leaf && !((sm >> (16 * q)) & 0xffffull)) m |= 0xffffull << (16 * q);
         }
+        if (root && only_slot >= 0) m &= 0xffffull << (16 * only_slot);
+        root = false;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (!((m >> (16 * q)) & 0xffffull)) continue;
@@ -1169,6 +1191,13 @@ static __device__ unsigned long long g_list_time[3][65536][4];
 // of 8 0.82 -> 0.67 ms; identical images
 #define YRT_BUNDLE_SUPER 1
 #endif
+#ifndef YRT_BUNDLE_FUSED
+// the super lists and the bundle lists in one launch (k_bundle_lists<true>). A/B in one process
+// (profiles/r6/ab/r6e_*): lists phase c4 0.31 -> 0.37 ms, instance100k 0.47 -> 0.60, c5 rank 0
+// of 8 0.82 -> 1.00, rank 0 of 8 0.10 -> 0.09; the block's four waves wait at its barrier for
+// the longest root slot's walk. Off.
+#define YRT_BUNDLE_FUSED 0
+#endif
 constexpr int super_bundles = 4;
 constexpr int super_max = 32;
 constexpr int super_list_f4 = 1 + 2 * super_max;  // {count} then {lo, word} {hi, 0} per leaf
@@ -1214,19 +1243,76 @@ __global__ __launch_bounds__(256) void k_bundle_super(dev_scene_view S, wf_buffe
 }
 
 // one wave per (bundle, light): the candidate list (see above) -- from the super-bundle's
-// list (YRT_BUNDLE_SUPER) or a walk of the tree -- as a chain of wide records
+// list (YRT_BUNDLE_SUPER) or a walk of the tree -- as a chain of wide records.
+// FUSED (YRT_BUNDLE_FUSED): one block per (super-bundle, light), wave w its bundle w, and the
+// super-bundle's list is built in the same launch: the four waves write their bundles' boxes to
+// LDS, each walks one root slot's subtree with the super-bundle's hull (the union box), and the
+// four shares, in slot order, are the super list every wave then filters -- k_bundle_super's
+// list, one launch and one wave's walk fewer
+template <bool FUSED>
 __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffers B, int n_items) {
     __shared__ float cand[4][bundle_max][8];  // per wave: lo.xyz, hi.xyz, word
+    __shared__ float scand[FUSED ? 4 : 1][super_max][8];  // FUSED: root slot w's share of the super list
+    __shared__ float sbox[FUSED ? 4 : 1][8];             // FUSED: bundle w's box, and whether it is bad
+    __shared__ int scount[4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nl = S.nlights;
     const int ngroups = (n_items + bundle_g - 1) / bundle_g;
-    const int gl = blockIdx.x * 4 + w;
-    if (gl >= ngroups * nl) return;  // (whole waves)
+    int g, li;
+    if constexpr (FUSED) {
+        const int nsuper = (ngroups + super_bundles - 1) / super_bundles;
+        if ((int)blockIdx.x >= nsuper * nl) return;  // (whole blocks)
+        const int sg = (int)blockIdx.x / nl;
+        li = (int)blockIdx.x - sg * nl, g = sg * super_bundles + w;
+    } else {
+        const int gl0 = blockIdx.x * 4 + w;
+        if (gl0 >= ngroups * nl) return;  // (whole waves)
+        g = gl0 / nl, li = gl0 - g * nl;
+    }
+    const int gl = g * nl + li;
     YRT_LT_STAMP(lt0);
-    const int g = gl / nl, li = gl - g * nl;
     float plx, ply, plz, phx, phy, phz;
     bool bad;
+    // (a bundle past the last, FUSED's padding: no items, an empty box)
     bundle_box(B, g * bundle_g, bundle_g, n_items, lane, plx, ply, plz, phx, phy, phz, bad);
+    int sc = -1;  // the super-bundle's list length, -1: walk the tree
+    const f4* sup = nullptr;
+    if constexpr (FUSED) {
+        const bool wbad = ballot(bad) != 0;
+        if (lane == 0) {
+            float* b = sbox[w];
+            b[0] = plx, b[1] = ply, b[2] = plz, b[3] = phx, b[4] = phy, b[5] = phz, b[6] = wbad ? 1.0f : 0.0f;
+        }
+        __syncthreads();
+        // the super-bundle's box: the union of its bundles' (bundle_box's fminf / fmaxf fold)
+        float Plx = INFINITY, Ply = INFINITY, Plz = INFINITY, Phx = -INFINITY, Phy = -INFINITY, Phz = -INFINITY;
+        bool sbad = false;
+        for (int q = 0; q < super_bundles; q++) {
+            const float* b = sbox[q];
+            Plx = fminf(Plx, b[0]), Ply = fminf(Ply, b[1]), Plz = fminf(Plz, b[2]);
+            Phx = fmaxf(Phx, b[3]), Phy = fmaxf(Phy, b[4]), Phz = fmaxf(Phz, b[5]);
+            sbad = sbad || b[6] != 0.0f;
+        }
+        vec3f Ls;
+        const bool lok = light_position(S, li, Ls);
+        int nq = -1;
+        if (!sbad && lok) {
+            if (!(Plx <= Phx)) {
+                nq = 0;
+            } else {
+                const hull_t Hs = make_hull(Plx, Ply, Plz, Phx, Phy, Phz, Ls, lane);
+                bool of;
+                hull_walk<super_max>(S, Hs, lane, scand[w], nq, of, w);
+                if (of) nq = -1;
+            }
+        }
+        if (lane == 0) scount[w] = nq;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's candidate stores
+        __syncthreads();
+        const int c0 = scount[0], c1 = scount[1], c2 = scount[2], c3 = scount[3];
+        sc = (c0 < 0 || c1 < 0 || c2 < 0 || c3 < 0 || c0 + c1 + c2 + c3 > super_max) ? -1 : c0 + c1 + c2 + c3;
+        if (g >= ngroups) return;  // (after the block's barriers)
+    }
     vec3f Lp;
     if (ballot(bad) || !light_position(S, li, Lp)) {
         if (lane == 0) B.lcount[gl] = -1;
@@ -1239,9 +1325,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
     const hull_t H = make_hull(plx, ply, plz, phx, phy, phz, Lp, lane);
     int nc = 0;
     bool overflow = false;
-    int sc = -1;  // the super-bundle's list length, -1: walk the tree
-    const f4* sup = nullptr;
-    if (YRT_BUNDLE_SUPER && bundle_g * super_bundles <= 256) {
+    if (!FUSED && YRT_BUNDLE_SUPER && bundle_g * super_bundles <= 256) {
         sup = B.slists + (size_t)((g / super_bundles) * nl + li) * super_list_f4;
         sc = __builtin_amdgcn_readfirstlane(__float_as_int(ld4(sup).x));
     }
@@ -1251,7 +1335,16 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         for (int c0 = 0; c0 < sc && !overflow; c0 += 4) {
             const int e = c0 + (lane >> 4);
             float4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-            if (e < sc) a = ld4(sup + 1 + 2 * e), b = ld4(sup + 2 + 2 * e);
+            if (e < sc) {
+                if constexpr (FUSED) {  // entry e of the four shares, in slot order
+                    int q = 0, k = e;
+                    while (k >= scount[q]) k -= scount[q], q++;
+                    const float* d = scand[q][k];
+                    a = {d[0], d[1], d[2], d[6]}, b = {d[3], d[4], d[5], 0.0f};
+                } else {
+                    a = ld4(sup + 1 + 2 * e), b = ld4(sup + 2 + 2 * e);
+                }
+            }
             const bool sep = e >= sc || hull_sep(H, a.x, a.y, a.z, b.x, b.y, b.z);
             const unsigned long long sm = ballot(sep);
             unsigned keep = 0;  // bit q: leaf c0 + q stays
@@ -2194,10 +2287,6 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         chunk_args C = {pix0, (int)std::min<long long>(pix_per_chunk, npix_total - pix0), spp, tiles_x};
         const int nsamp = C.npix * spp;
         const int grid = (nsamp + WF_BLOCK - 1) / WF_BLOCK;
-        if (nlevels > 1) {
-            hipError_t e = hipMemsetAsync(B.count, 0, count_bytes(nlevels), stream);
-            if (e != hipSuccess) return e;
-        }
         constexpr int TB = shadow_block<PACKET>();
         const int tgrid = (nsamp + TB - 1) / TB;
         // level 0's shadow rays run on the persistent any-hit grid (k_shadow_persist) -- on
@@ -2217,18 +2306,22 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         B.cam_lists = cam_lists_possible && lists;
         B.bundles = bundles_possible && lists;
         ds.last_camera_lists |= B.cam_lists != 0, ds.last_bundles |= B.bundles != 0;
-        if ((B.cam_lists || B.bundles) && !list_stats) {
-            list_stats = true;
-            hipError_t e = hipMemsetAsync(B.lstats, 0, 4 * sizeof(unsigned long long), stream);
-            if (e != hipSuccess) return e;
-        }
+        const bool zero_lstats = (B.cam_lists || B.bundles) && !list_stats;
+        list_stats |= zero_lstats;
         int t = T.begin(phase_lists, stream);
-        if (PACKET && pix0 == 0) {
-            // the camera-relative instance-level records of this render (timed in the lists
-            // phase, YRT_PHASE_LISTS, with the camera lists built from them)
-            const int nrec = (int)ds.ntnodes * 2 * spine_len;
-            hipLaunchKernelGGL(k_relative_records, dim3((nrec + WF_BLOCK - 1) / WF_BLOCK), dim3(WF_BLOCK), 0, stream,
-                               ds.view.tpair, nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel);
+        {
+            // the chunk's setup (k_chunk_setup): the camera-relative instance-level records of
+            // this render (the first chunk of a packet render; timed in the lists phase,
+            // YRT_PHASE_LISTS, with the camera lists built from them) and the chunk's zeroed
+            // counters
+            const int nrec = (PACKET && pix0 == 0) ? (int)ds.ntnodes * 2 * spine_len : 0;
+            const int count_ints = nlevels > 1 ? (int)(count_bytes(nlevels) / sizeof(int)) : 0;
+            const int counter_words = pix0 == 0 && counters ? cnt_slots * cnt_count : 0;
+            const int work = std::max(std::max(nrec, count_ints), std::max(counter_words, 32));
+            const int nb = std::min((work + WF_BLOCK - 1) / WF_BLOCK, 1024);
+            hipLaunchKernelGGL(k_chunk_setup, dim3(nb), dim3(WF_BLOCK), 0, stream, nrec ? ds.view.tpair : nullptr,
+                               nrec, A.cam.ox, A.cam.oy, A.cam.oz, ds.trel, B.queue,
+                               zero_lstats ? B.lstats : nullptr, B.count, count_ints, counters, counter_words);
         }
         if (B.cam_lists) {
             const int nt = C.npix / (TILE * TILE);
@@ -2239,9 +2332,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         bool persist = false;
         if constexpr (!COUNT && PACKET) {
             persist = ((long long)nsamp + 63) / 64 >= (long long)YRT_PRIMARY_PERSIST_MIN_ITEMS;
-            if (persist) {
-                hipError_t e = hipMemsetAsync(B.queue + 16, 0, 9 * sizeof(unsigned), stream);
-                if (e != hipSuccess) return e;
+            if (persist) {  // (its work counters B.queue[16, 25) were zeroed by k_chunk_setup)
                 const int nb = ds.num_cus * (YRT_PRIMARY_WAVES * 4 * 64 / YRT_PRIMARY_SP_BLOCK);
                 if (B.cam_lists)
                     hipLaunchKernelGGL((k_primary_persist<SE, 0, true>), dim3(nb), dim3(YRT_PRIMARY_SP_BLOCK), 0,
@@ -2286,14 +2377,20 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 dim3 sg(level ? stride_grid * WF_BLOCK / TB : tgrid, ds.nlights);
                 if (level == 0 && shadow_persist && B.bundles) {  // the bundles' candidate lists
                     t = T.begin(phase_lists, stream);
-                    if (YRT_BUNDLE_SUPER) {
+                    if (YRT_BUNDLE_FUSED && YRT_BUNDLE_SUPER && bundle_g * super_bundles <= 256) {
                         const long long ns = (long long)super_count(nsamp) * ds.nlights;
-                        hipLaunchKernelGGL(k_bundle_super, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, stream, ds.view,
-                                           B, tgrid);
+                        hipLaunchKernelGGL(k_bundle_lists<true>, dim3((unsigned)ns), dim3(256), 0, stream, ds.view, B,
+                                           tgrid);
+                    } else {
+                        if (YRT_BUNDLE_SUPER) {
+                            const long long ns = (long long)super_count(nsamp) * ds.nlights;
+                            hipLaunchKernelGGL(k_bundle_super, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, stream,
+                                               ds.view, B, tgrid);
+                        }
+                        const long long nw = (long long)bundle_count(nsamp) * ds.nlights;
+                        hipLaunchKernelGGL(k_bundle_lists<false>, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream,
+                                           ds.view, B, tgrid);
                     }
-                    const long long nw = (long long)bundle_count(nsamp) * ds.nlights;
-                    hipLaunchKernelGGL(k_bundle_lists, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream, ds.view, B,
-                                       tgrid);
                     T.end(t, stream);
                 }
                 t = T.begin(phase_shadow, stream);
@@ -2301,11 +2398,8 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
                 // hardware's dealing (shadow 1.64 -> 1.72 ms with them persistent)
                 if (level == 0 && shadow_persist) {
                     // one resident grid: two 1024-thread blocks per CU (8 waves per SIMD)
+                    // (its work counters B.queue[0, 9) were zeroed by k_chunk_setup)
                     const int nb = ds.num_cus * (YRT_SHADOW_WAVES * 4 * 64 / SP_BLOCK);
-                    {
-                        hipError_t e = hipMemsetAsync(B.queue, 0, 9 * sizeof(unsigned), stream);
-                        if (e != hipSuccess) return e;
-                    }
                     constexpr int L = YRT_SHADOW_LDS_RECORDS;
                     if (stage && L > 0 && ds.view.nwtop >= L) {  // (the copy reads L whole records)
                         hipLaunchKernelGGL((k_shadow_persist<L>), dim3(nb), dim3(SP_BLOCK), 0, stream, ds.view,
