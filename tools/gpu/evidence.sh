@@ -1,6 +1,6 @@
 #!/bin/bash
 # One round's evidence set on one GPU box, in parts (each well under gpurun's 20-minute
-# limit), collected once at the round's final build (ROUND=r5 by default):
+# limit), collected once at the round's final build (ROUND=r6 by default):
 #   bash tools/gpu/evidence.sh A TAG   -m gpu suite, smoke, c4 counters + kernel stats, the
 #                                    default bench line (the three CPU legs), N=2 rehearsal
 #   bash tools/gpu/evidence.sh B TAG   c3 and c5 counters + bench lines
@@ -13,7 +13,7 @@
 # summaries (stamped with libyrt.so's code identity) go to this copy's profiles/ and to
 # gpurun_out/TAG/, so the bench lines that follow carry the issue roofline.
 set -u
-PART=$1; TAG=$2; ROUND=${ROUND:-r5}
+PART=$1; TAG=$2; ROUND=${ROUND:-r6}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 run() { "$@"; local rc=$?; if [ $rc -ne 0 ]; then echo "FAILED (rc=$rc): $*"; exit $rc; fi; }
@@ -46,6 +46,7 @@ elif [ "$PART" = B ]; then
   run timeout -k 10 400 python bench.py --resolution 4096 --width 4096 --samples 16 --steps 2 --warmup 1 --cpu-seconds 6 > $OUT/bench_c5_1gpu.json 2> $OUT/c5.err
   cut -c1-300 $OUT/bench_c3_refl.json $OUT/bench_c5_1gpu.json
 elif [ "$PART" = C ]; then
+  run timeout -k 10 300 python tools/rank_share.py > $OUT/rank_share_c4.json 2> $OUT/rank_share.err
   for n in 2 4 8; do
     pmc pmc_c4_r0of$n 150 --profile-rank 0/$n
     summ instance10000-1920x1080-s8-n$n-wavefront $OUT/pmc_c4_r0of$n

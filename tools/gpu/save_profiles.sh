@@ -2,9 +2,9 @@
 # Copy one tools/gpu/evidence.sh run's evidence from gpurun_out/TAG into
 # profiles/ROUND/TAG: bench lines, logs, counter CSVs, kernel stats and summaries (the
 # run's raw rocprofv3 output directories stay in gpurun_out/).
-#   bash tools/gpu/save_profiles.sh TAG [ROUND]     (ROUND: r5 by default)
+#   bash tools/gpu/save_profiles.sh TAG [ROUND]     (ROUND: r6 by default)
 set -eu
-TAG=$1; ROUND=${2:-r5}
+TAG=$1; ROUND=${2:-r6}
 S=gpurun_out/$TAG; D=profiles/$ROUND/$TAG
 mkdir -p $D
 for f in $S/*.json $S/pytest*.log $S/smoke.log; do [ -e "$f" ] && cp "$f" $D/; done

@@ -40,7 +40,7 @@ def code_identity(lib: Path) -> str:
 PHASE_OF = {"k_primary": "primary", "k_primary_persist": "primary", "k_shadow": "shadow",
             "k_shadow_persist": "shadow", "k_shade": "shade", "k_bounce": "bounce",
             "k_fold_children": "fold", "k_accumulate": "accumulate", "render_kernel": "megakernel",
-            "k_relative_records": "lists", "k_chunk_setup": "lists", "k_bundle_fused": "lists", "k_camera_lists": "lists", "k_bundle_lists": "lists", "k_list_stats": "lists"}
+            "k_relative_records": "lists", "k_chunk_setup": "lists", "k_bundle_super": "lists", "k_camera_lists": "lists", "k_bundle_lists": "lists", "k_list_stats": "lists"}
 
 
 def short(name: str) -> str:
