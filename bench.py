@@ -355,12 +355,36 @@ def issue_roofline(issue_json: Path, key: str, kernel_ms: float, identity: str, 
     return bound, pipes, rec
 
 
-def roofline_phase(phases: dict) -> str:
-    """the phase whose kernel the line's roofline describes: the longest of this frame's
-    per-ray phases ({phase: (ms, launches)}), never a fixed per-render phase (FIXED_PHASES)"""
+def roofline_phase(phases: dict, n1_cycles: dict | None = None) -> str:
+    """the phase whose kernel the line's roofline describes, among this frame's per-ray phases
+    ({phase: (ms, launches)}; never a fixed per-render phase, FIXED_PHASES): the one that
+    dominates the same workload at N = 1 (its cycles per launch in the committed counters,
+    n1_ranking(), times its launches), so that an N-rank line -- whose phases can be contended
+    or latency-bound at a small share -- reports the kernel the N = 1 line does; without N = 1
+    counters, the longest phase of this run"""
     per_ray = {k: v for k, v in phases.items() if k not in FIXED_PHASES and v[1] > 0}
     pool = per_ray or phases
+    # (cycles per launch at N = 1 x this run's launches: a phase's launches per frame are the
+    # workload's, whatever the rank count)
+    ranked = {k: n1_cycles[k] * pool[k][1] for k in pool if n1_cycles and k in n1_cycles}
+    if ranked:
+        return max(ranked, key=ranked.get)
     return max(pool, key=lambda k: pool[k][0])
+
+
+def n1_ranking(issue_json: Path, prefix: str, identity: str) -> dict:
+    """{phase: GPU cycles per launch} of the workload at N = 1 from the committed counters
+    (keys prefix + phase, prefix = scene-WxH-s<samples>-n1-<algorithm>-), only records of the
+    timed library's code identity"""
+    try:
+        table = json.loads(Path(issue_json).read_text())
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for k, rec in table.items():
+        if k.startswith(prefix) and rec.get("code_identity") == identity and rec.get("cycles"):
+            out[k[len(prefix):]] = float(rec["cycles"])
+    return out
 
 
 def digest_key(scene: str, W: int, H: int, samples: int) -> str:
@@ -492,7 +516,12 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ds.last_stats()
     phases = ds.last_timings()  # {phase: (ms over the K steps, launches)}
-    dom = roofline_phase(phases)
+    try:
+        identity = code_identity(yrt_native.LIB_PATH)
+    except (OSError, ValueError, subprocess.CalledProcessError) as e:  # no binutils/bundler: no roofline
+        identity = f"unavailable ({type(e).__name__})"
+    dom = roofline_phase(phases, n1_ranking(Path(a.issue_json), f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-",
+                                            identity))
     dom_ms = phases[dom][0] / a.steps  # per frame
     dom_launches = phases[dom][1] / a.steps
     render_ms = sum(v[0] for v in phases.values()) / a.steps
@@ -550,10 +579,6 @@ def main():
         metric = BASELINE_METRIC if is_c4 else f"Mrays/sec + ms/frame, {a.scene} {W}×{H}×{spp}spp, {world} MI355X"
         key = f"{a.scene}-{W}x{H}-s{a.samples}-n{band_world}-{a.algorithm}-{dom}"
         kernel_ms = dom_ms / dom_launches
-        try:
-            identity = code_identity(yrt_native.LIB_PATH)
-        except (OSError, ValueError, subprocess.CalledProcessError) as e:  # no binutils/bundler: no roofline
-            identity = f"unavailable ({type(e).__name__})"
         tr, _ = load_counters(Path(a.traffic_json), key, identity)
         traffic = tr.get("hbm_bytes_per_launch") if tr else None
         key_n1 = f"{a.scene}-{W}x{H}-s{a.samples}-n1-{a.algorithm}-{dom}"

@@ -92,6 +92,27 @@ def test_roofline_phase_is_a_per_ray_phase():
     # a phase with no launch is never picked; with nothing but fixed phases, the longest
     assert b.roofline_phase({"primary": (0.0, 0), "megakernel": (3.0, 1), "lists": (9.0, 1)}) == "megakernel"
     assert b.roofline_phase({"lists": (0.2, 2)}) == "lists"
+    # with the N = 1 counters of the workload, their ranking decides: the round-6 N = 2
+    # rehearsal timed shadow 7.58 / primary 6.55 ms (two ranks on one card), N = 1 ranks the
+    # closest hit first (9.28 vs 8.38 ms per launch)
+    contended = {"primary": (6.55, 3), "shadow": (7.58, 3), "shade": (3.12, 3), "lists": (3.81, 9)}
+    n1 = {"primary": 2.23e7, "shadow": 2.01e7, "shade": 4.2e6, "lists": 1.8e5}
+    assert b.roofline_phase(contended) == "shadow"
+    assert b.roofline_phase(contended, n1) == "primary"
+    assert b.roofline_phase(contended, {"bounce": 1.0}) == "shadow"  # no N = 1 record of these phases
+
+
+def test_n1_ranking_reads_only_the_timed_build(tmp_path):
+    b = _bench_module()
+    f = tmp_path / "issue.json"
+    pre = "instance10000-1920x1080-s8-n1-wavefront-"
+    f.write_text(json.dumps({pre + "primary": {"cycles": 2.2e7, "code_identity": "a" * 64},
+                             pre + "shadow": {"cycles": 2.0e7, "code_identity": "a" * 64},
+                             pre + "shade": {"cycles": 4.0e6, "code_identity": "b" * 64},
+                             "instance10000-1920x1080-s8-n2-wavefront-primary": {"cycles": 1.1e7,
+                                                                                 "code_identity": "a" * 64}}))
+    assert b.n1_ranking(f, pre, "a" * 64) == {"primary": 2.2e7, "shadow": 2.0e7}
+    assert b.n1_ranking(tmp_path / "missing.json", pre, "a" * 64) == {}
 
 
 def test_frame_matches_n1(tmp_path):

@@ -30,7 +30,7 @@ TIMED = {
     "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 39),
     "k_camera_lists": (r"k_camera_lists", 0, 0, 0),
     # (the list builders' 28 private bytes: a 7-float slot record indexed per lane, not spills)
-    "k_bundle_lists": (r"k_bundle_lists", 0, 28, 0),
+    "k_bundle_lists": (r"k_bundle_listsILb0EE", 0, 28, 0),
     "k_bundle_super": (r"k_bundle_super", 0, 28, 0),
     # the LDS-staged walks (yrt_scene_set_lds_staging): 511 camera-relative spine records
     # (32 KiB) beside the parked 1/d, and 85 wide records; two 1024-thread blocks per CU must
