@@ -215,6 +215,11 @@ int yrt_scene_set_tile_lists(yrt_scene* ds, int mode);
  * entries, bundle lists} of the last render that built lists (a list that fell back to the
  * tree counts as its capacity + 1) */
 int yrt_scene_tile_lists(yrt_scene* ds, int* camera_on, int* bundles_on, unsigned long long* sums);
+/* the instances the lists' masks excluded in the last render that built lists (synchronises
+ * with it): excluded[0] = over every camera list's leaves, the instances whose world box the
+ * tile's cone excludes; excluded[1] = the same over every shadow bundle's list and its hull
+ * (instance masks; the walks pass over them, identical images) */
+int yrt_scene_tile_list_masks(yrt_scene* ds, unsigned long long* excluded);
 /* LDS staging of the instance tree's hot top (the north_star's "hot node tiles staged in LDS";
  * DESIGN.md §5). on = 1: yrt_render's persistent closest-hit grid copies the first 511
  * camera-relative spine records, and its persistent any-hit grid the first 85 4-wide records

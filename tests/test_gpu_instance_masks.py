@@ -11,12 +11,15 @@ has to get right:
   the walk reuses the world tmax along the renormalised local direction);
 - instances whose shape sits far from its local origin, and a shape with an empty BVH;
 - dense clusters, so that leaves hold several instances and rays pass between them;
-- a camera inside the instance cloud and one far outside it, and lights among the
+- a camera inside the instance cloud, one far outside it, one far away with a narrow view of
+  the dense cluster (its tiles' lists reach single leaves), and lights among the
   instances.
 
 Each frame is rendered with the lists forced on (masks built) and off (no lists, no masks);
 both must be bit-identical and equal the oracle (the reference's raytrace(),
-raytrace.cpp:213-254, through the C restatement)."""
+raytrace.cpp:213-254, through the C restatement). The masks must also have fired: the lists
+report how many instances their cones and hulls excluded (yrt_scene_tile_list_masks), and a
+test whose masks never excluded anything would not test them."""
 from __future__ import annotations
 
 import numpy as np
@@ -50,11 +53,13 @@ def _frame(R, o):
     return np.r_[R[:, 0], R[:, 1], R[:, 2], o].astype(np.float32)
 
 
-def _mask_scene(yrt, tmp_path, far_camera):
+def _mask_scene(yrt, tmp_path, camera):
     rng = np.random.default_rng(17)
     s = yrt.Scene.create()
-    if far_camera:
+    if camera == "far":
         s.add_camera(_frame(_rot(0, -0.5), [0.0, 60.0, 110.0]), fovy=0.25, aspect=16 / 9, focus=120.0)
+    elif camera == "zoom":  # far away with a narrow view of the dense cluster: a tile's cone meets few leaves
+        s.add_camera(_frame(_rot(0, -0.56), [2.0, 40.0, 60.0]), fovy=0.06, aspect=16 / 9, focus=74.0)
     else:  # inside the cloud
         s.add_camera(_frame(_rot(1, 0.3) @ _rot(0, -0.2), [1.0, 2.5, 6.0]), fovy=1.0, aspect=16 / 9, focus=8.0)
     mats = [s.add_material(kd=(0.6, 0.5, 0.4)),
@@ -93,15 +98,15 @@ def _mask_scene(yrt, tmp_path, far_camera):
     for o in ([-6, 9, -4], [8, 12, 5], [1.5, 1.2, -2.5]):  # the last one among the instances
         lm = s.add_material(ke=(40.0, 35.0, 30.0))
         s.add_instance(_frame(np.eye(3), o), pt, lm)
-    path = tmp_path / f"masks_{int(far_camera)}.yrtscene"
+    path = tmp_path / f"masks_{camera}.yrtscene"
     s.save(str(path))
     yrt.build_bvh(s)
     return s, path
 
 
-@pytest.mark.parametrize("far_camera", [False, True])
-def test_instance_masks_on_off_equal_oracle(yrt, tmp_path, far_camera):
-    s, path = _mask_scene(yrt, tmp_path, far_camera)
+@pytest.mark.parametrize("camera", ["near", "far", "zoom"])
+def test_instance_masks_on_off_equal_oracle(yrt, tmp_path, camera):
+    s, path = _mask_scene(yrt, tmp_path, camera)
     ds = s.upload(0)
     res, spp = 96, 4
     out = {}
@@ -110,13 +115,20 @@ def test_instance_masks_on_off_equal_oracle(yrt, tmp_path, far_camera):
         img, st = yrt.raytrace(ds, (0.1, 0.1, 0.1), res, spp, return_stats=True)
         out[mode] = (img, st, ds.tile_lists())
     (on, st_on, l_on), (off, st_off, _) = out["on"], out["off"]
-    print(f"far_camera={far_camera}: lists on {l_on}")
+    print(f"camera={camera}: lists on {l_on}")
     assert l_on["camera"] and l_on["bundles"], l_on
+    # the masks excluded instances (else the on/off comparison proves nothing): the bundles' in
+    # every frame; the camera lists' in the zoomed view, whose tiles' cones reach single leaves
+    # (in the near and far views every tile's cone meets more leaves than a list holds, its
+    # frontier is 32 subtrees, and only a listed leaf carries skip bits)
+    assert l_on["bundle_instances_masked"] > 0, l_on
+    if camera == "zoom":
+        assert l_on["camera_instances_masked"] > 0 and l_on["camera_entries"] < 32 * l_on["camera_lists"], l_on
     np.testing.assert_array_equal(on.view(np.uint32), off.view(np.uint32))
     assert st_on == st_off and st_on["shadow_rays"] > 0
     ref, n, trunc = Oracle(str(path)).render(res, spp)
     assert trunc == 0 and n == st_on["rays"]
     differ = int(np.sum(on.view(np.uint32) != ref.view(np.uint32)))
-    print(f"far_camera={far_camera}: {differ} of {on.size} channels not bit-exact vs oracle")
+    print(f"camera={camera}: {differ} of {on.size} channels not bit-exact vs oracle")
     assert close_mask(on, ref).all()
     assert np.mean(on.view(np.uint32) == ref.view(np.uint32)) > 0.99

@@ -170,7 +170,8 @@ def test_tile_lists_argument_errors(yrt):
     ds = yrt.DeviceScene(host(yrt, "instance1k"), 0)  # a handle of its own (upload() caches one)
     # a handle that has not rendered, and one whose renders never built lists, read back zeros
     assert ds.tile_lists() == {"camera": False, "bundles": False, "camera_entries": 0, "camera_lists": 0,
-                               "bundle_entries": 0, "bundle_lists": 0}
+                               "bundle_entries": 0, "bundle_lists": 0, "camera_instances_masked": 0,
+                               "bundle_instances_masked": 0}
     ds.set_tile_lists("off")
     yrt.raytrace(ds, (0.1, 0.1, 0.1), 90, 2)
     assert ds.tile_lists()["camera"] is False and ds.tile_lists()["camera_lists"] == 0

@@ -40,6 +40,7 @@ def test_null_handles_are_status_codes(yrt):
     assert lib.yrt_scene_set_tile_lists(None, 0) == 1
     assert lib.yrt_scene_set_trace_algorithm(None, 0) == 1
     assert lib.yrt_scene_tile_lists(None, None, None, None) == 1
+    assert lib.yrt_scene_tile_list_masks(None, None) == 1
     assert lib.yrt_scene_set_lds_staging(None, 1) == 1
     assert lib.yrt_scene_lds_staging(None, None) == 1
 

@@ -191,8 +191,11 @@ class DeviceScene:
         """the lists the last render used, and the sums of the last render that built any"""
         cam, bun, sums = C.c_int(), C.c_int(), (C.c_ulonglong * 4)()
         check(N.lib.yrt_scene_tile_lists(self._h, C.byref(cam), C.byref(bun), sums), "tile_lists")
+        ex = (C.c_ulonglong * 2)()
+        check(N.lib.yrt_scene_tile_list_masks(self._h, ex), "tile_list_masks")
         return {"camera": bool(cam.value), "bundles": bool(bun.value), "camera_entries": int(sums[0]),
-                "camera_lists": int(sums[1]), "bundle_entries": int(sums[2]), "bundle_lists": int(sums[3])}
+                "camera_lists": int(sums[1]), "bundle_entries": int(sums[2]), "bundle_lists": int(sums[3]),
+                "camera_instances_masked": int(ex[0]), "bundle_instances_masked": int(ex[1])}
 
     def set_lds_staging(self, on: bool) -> None:
         """LDS staging of the instance tree's top in render_into's persistent walks (the tile

@@ -120,6 +120,7 @@ _sig = {
     "yrt_scene_set_trace_algorithm": (C.c_int, [_vp, C.c_int]),
     "yrt_scene_set_tile_lists": (C.c_int, [_vp, C.c_int]),
     "yrt_scene_tile_lists": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_ulonglong)]),
+    "yrt_scene_tile_list_masks": (C.c_int, [_vp, C.POINTER(C.c_ulonglong)]),
     "yrt_scene_set_lds_staging": (C.c_int, [_vp, C.c_int]),
     "yrt_scene_lds_staging": (C.c_int, [_vp, C.POINTER(C.c_int)]),
     "yrt_last_stats": (C.c_int, [_vp, C.POINTER(Stats)]),

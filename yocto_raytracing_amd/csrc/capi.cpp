@@ -421,6 +421,17 @@ int yrt_scene_tile_lists(yrt_scene* s, int* camera_on, int* bundles_on, unsigned
     });
 }
 
+int yrt_scene_tile_list_masks(yrt_scene* s, unsigned long long* excluded) {
+    if (!s || !excluded) return YRT_ERR_INVALID_ARG;
+    return guarded([&] {
+        yrt::device_scene& ds = *s->ds;
+        hip_check(hipSetDevice(ds.device), "hipSetDevice");
+        if (ds.list_stats_ev && ds.list_stats_recorded) hip_check(hipEventSynchronize(ds.list_stats_ev), "list sums");
+        for (int i = 0; i < 2; i++) excluded[i] = ds.list_stats_host ? ds.list_stats_host[4 + i] : 0;
+        return YRT_OK;
+    });
+}
+
 int yrt_scene_set_lds_staging(yrt_scene* s, int on) {
     if (!s || (on != 0 && on != 1)) return YRT_ERR_INVALID_ARG;
     s->ds->lds_staging = on;

@@ -67,6 +67,11 @@ constexpr int shadow_block() { return PACKET ? YRT_SHADOW_BLOCK : WF_BLOCK; }
 constexpr int CHUNK_LOG2 = 29;  // samples per chunk, non-reflective scenes (~70 B of HBM each)
 constexpr int TILE = 8;         // pixel tiles of TILE x TILE in the sample enumeration
 
+// the render's list sums (k_list_stats, yrt_scene_tile_lists / yrt_scene_tile_list_masks):
+// camera-list entries, camera lists, bundle-list entries, bundle lists, then the instances the
+// camera lists' and the bundle lists' masks exclude
+constexpr int list_sums = 6;
+
 struct wf_buffers {
     f4* surf0;          // {p.xyz, info}: info = mat*4+kind, -1 miss, -2 not a sample
     f4* surf1;          // {n.xyz, u}
@@ -95,13 +100,15 @@ struct wf_buffers {
     int bundles;            // 1: this chunk's k_primary writes pbox and its shadow items walk lists
     f4* pbox;               // per 64-sample item: {lo.xyz, -1 if a hit point is not finite} {hi.xyz, -}
     int* lcount;            // per (bundle, light): candidate leaves, -1 = walk the tree
+    int* lskip;             // per (bundle, light): instances of its listed leaves its hull excludes
     f4* lists;              // per (bundle, light): bundle_recs wide records (wide_record_bytes each)
     f4* slists;             // per (super-bundle, light): a leaf list (YRT_BUNDLE_SUPER)
     // camera lists (the closest hit of the camera rays, k_camera_lists)
     int cam_lists;          // 1: this chunk's camera rays walk their tile's list
     int* ccount;            // per 8x8-pixel tile of the chunk: listed leaves, -1 = walk the tree
+    int* cskip;             // per tile: instances of its listed leaves its cone excludes
     f4* clist;              // per tile: camera_list_max entries of 2 f4 {lo - o, first} {hi - o, count}
-    unsigned long long* lstats;  // the render's list sums (k_list_stats)
+    unsigned long long* lstats;  // the render's list sums (k_list_stats, list_sums of them)
 };
 
 // Mirror levels are compacted into level_segments segments of B.seg slots: segment g of
@@ -669,7 +676,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_chunk_setup(const f4* __restrict__
             trel[k] = {r.x - ox, r.y - oy, r.z - oz, r.w};
         }
     if (i < 32) queue[i] = 0u;
-    if (lstats && i < 4) lstats[i] = 0ull;
+    if (lstats && i < list_sums) lstats[i] = 0ull;
     for (int k = i; k < count_ints; k += stride) count[k] = 0;
     if (counters)
         for (int k = i; k < counter_words; k += stride) counters[k] = 0ull;
@@ -1315,11 +1322,11 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
     }
     vec3f Lp;
     if (ballot(bad) || !light_position(S, li, Lp)) {
-        if (lane == 0) B.lcount[gl] = -1;
+        if (lane == 0) B.lcount[gl] = -1, B.lskip[gl] = 0;
         return;
     }
     if (!(plx <= phx)) {  // no hit point in the bundle: no shadow ray
-        if (lane == 0) B.lcount[gl] = 0;
+        if (lane == 0) B.lcount[gl] = 0, B.lskip[gl] = 0;
         return;
     }
     const hull_t H = make_hull(plx, ply, plz, phx, phy, phz, Lp, lane);
@@ -1365,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         hull_walk<bundle_max>(S, H, lane, cand[w], nc, overflow);
     }
     if (overflow) {
-        if (lane == 0) B.lcount[gl] = -1;
+        if (lane == 0) B.lcount[gl] = -1, B.lskip[gl] = 0;
         return;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the candidate stores, before any lane reads them
@@ -1399,6 +1406,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
     // (dev_scene_view ibox) outside a hull plane by more than the margin fail every ray's
     // root box test in the instance's space, so the walk skips them (skip bits in the leaf's
     // word: the bundle records' format, bundle_leaf_word)
+    int nskip = 0;  // (wave-uniform) instances the hull excludes, over the listed leaves
     if (YRT_INSTANCE_MASKS && S.inst_masks) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         for (int e = 0; e < nc; e++) {
@@ -1417,6 +1425,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
                     if (i0 + q < count && ((sm >> (16 * q)) & 0xffffull)) skip |= 1u << (i0 + q);
             }
             if (lane == 0) cand[w][e][6] = __uint_as_float(bundle_leaf_word(first, count, skip));
+            nskip += __popc(skip);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // a leaf whose every instance is excluded leaves the list (the walk would test its box
@@ -1477,7 +1486,7 @@ __global__ __launch_bounds__(256) void k_bundle_lists(dev_scene_view S, wf_buffe
         float4 o = row < 7 ? make_float4(a[row], a[8 + row], a[16 + row], a[24 + row]) : make_float4(0, 0, 0, 0);
         reinterpret_cast<float4*>(B.lists)[(size_t)(rec0 + rq) * 8 + row] = o;
     }
-    if (lane == 0) B.lcount[gl] = nc;
+    if (lane == 0) B.lcount[gl] = nc, B.lskip[gl] = nskip;
     YRT_LT_STAMP(lt3);
     YRT_LT_WRITE(2, gl, lt1 - lt0, lt2 - lt1, lt3 - lt2, (unsigned long long)(unsigned)nc);
 }
@@ -1531,14 +1540,11 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
                      (u - 0.5f) * Kc.w * Kc.xz + (v - 0.5f) * Kc.h * Kc.yz - Kc.focus * Kc.zz};
     };
     const vec3f O = {Kc.ox, Kc.oy, Kc.oz};
-    // the scene's extent (the absolute root box) and the origin, for the margin
-    float M = fmaxf(fmaxf(fabsf(O.x), fabsf(O.y)), fabsf(O.z));
-    {
-        const float4 rl = ld4(S.tpair), rh = ld4(S.tpair + 1);
-        M = fmaxf(M, fmaxf(fmaxf(fmaxf(fabsf(rl.x), fabsf(rl.y)), fmaxf(fabsf(rl.z), fabsf(rh.x))),
-                           fmaxf(fabsf(rh.y), fabsf(rh.z))));
-    }
-    const float eps = 1e-3f + 3e-5f * M;
+    // the margin of a box: 1e-3 + 3e-5 x the magnitude of its coordinates and the origin's, far
+    // above the slab test's rounding at that magnitude. Per box, not the scene's: the root box's
+    // magnitude made it huge for every box once one instance was (an instance of an empty shape
+    // is bounded by +-FLT_MAX), and every list became the whole tree.
+    const float Om = fmaxf(fmaxf(fabsf(O.x), fabsf(O.y)), fabsf(O.z));
     // cone plane k (through O and corners k, k + 1; the cone on its negative side), computed by
     // lane k < 4 and read by every lane
     vec3f n = {0, 0, 0};
@@ -1549,20 +1555,24 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
         const vec3f c = dir(0.5f * (u0 + u1), 0.5f * (v0 + v1));
         if (dot(n, c) > 0.0f) n = n * -1.0f;
     }
-    float pn[4][3], pm[4];
+    float pn[4][3], pl1[4];
     for (int k = 0; k < 4; k++) {
         pn[k][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(n.x), k));
         pn[k][1] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(n.y), k));
         pn[k][2] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(n.z), k));
-        pm[k] = (fabsf(pn[k][0]) + fabsf(pn[k][1]) + fabsf(pn[k][2])) * eps;
+        pl1[k] = fabsf(pn[k][0]) + fabsf(pn[k][1]) + fabsf(pn[k][2]);
     }
-    // a camera-relative box outside some cone plane (a NaN bound never separates)
+    // a camera-relative box outside some cone plane by more than its margin (a NaN bound never
+    // separates; neither does an infinite one, whose margin is infinite)
     auto outside = [&](float4 lo, float4 hi) {
+        const float Mb = Om + fmaxf(fmaxf(fmaxf(fabsf(lo.x), fabsf(lo.y)), fmaxf(fabsf(lo.z), fabsf(hi.x))),
+                                    fmaxf(fabsf(hi.y), fabsf(hi.z)));
+        const float eps = 1e-3f + 3e-5f * Mb;
         bool o = false;
         for (int k = 0; k < 4; k++) {
             const float mn = pn[k][0] * (pn[k][0] > 0.0f ? lo.x : hi.x) + pn[k][1] * (pn[k][1] > 0.0f ? lo.y : hi.y) +
                              pn[k][2] * (pn[k][2] > 0.0f ? lo.z : hi.z);
-            o = o || mn > pm[k];
+            o = o || mn > pl1[k] * eps;
         }
         return o;
     };
@@ -1639,6 +1649,7 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
     YRT_LT_STAMP(lt2);
     float4 elo = {0, 0, 0, 0}, ehi = {0, 0, 0, 0};
     bool keep = false;
+    int nskip = 0;  // this lane's entry: the instances the cone excludes
     if (lane < nf) {
         const float4 lo = fr[w][cur][lane][0];
         float4 hi = fr[w][cur][lane][1];
@@ -1657,6 +1668,7 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
                 if (outside(ar, br)) skip |= 1u << i;
             }
             hi.w = __uint_as_float(cw | skip << 16);
+            nskip = __popc(skip);
             // a leaf whose every instance is excluded leaves the list
             keep = skip != (1u << count) - 1u;
         } else {
@@ -1672,34 +1684,35 @@ __global__ __launch_bounds__(256) void k_camera_lists(dev_scene_view S, dev_rend
         out[1] = {ehi.x, ehi.y, ehi.z, ehi.w};
     }
     nf = __popcll(km);
-    if (lane == 0) B.ccount[t] = nf;
+    nskip = (int)wave_sum((unsigned long long)nskip);
+    if (lane == 0) B.ccount[t] = nf, B.cskip[t] = nskip;
     YRT_LT_STAMP(lt3);
     YRT_LT_WRITE(0, t, lt1 - lt0, lt2 - lt1, lt3 - lt2, (unsigned long long)nrounds << 32 | (unsigned)nf);
 }
 
 // the sums of one chunk's list lengths into B.lstats (a list that fell back to the tree counts
-// as camera_list_max + 1 / bundle_max + 1 entries), added to the render's totals: a grid-stride
-// sum per block, four atomics per block
+// as camera_list_max + 1 / bundle_max + 1 entries) and of the instances the lists' masks
+// exclude, added to the render's totals: a grid-stride sum per block, list_sums atomics per block
 __global__ __launch_bounds__(256) void k_list_stats(wf_buffers B, int ntiles, int nlists) {
-    __shared__ unsigned long long part[4][256 / 64];
-    unsigned long long v[4] = {0, 0, 0, 0};
+    __shared__ unsigned long long part[list_sums][256 / 64];
+    unsigned long long v[list_sums] = {};
     const int stride = gridDim.x * 256;
     if (B.cam_lists)
         for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < ntiles; i += stride) {
             const int n = B.ccount[i];
-            v[0] += n < 0 ? camera_list_max + 1 : n, v[1]++;
+            v[0] += n < 0 ? camera_list_max + 1 : n, v[1]++, v[4] += (unsigned)B.cskip[i];
         }
     if (B.bundles)
         for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < nlists; i += stride) {
             const int n = B.lcount[i];
-            v[2] += n < 0 ? bundle_max + 1 : n, v[3]++;
+            v[2] += n < 0 ? bundle_max + 1 : n, v[3]++, v[5] += (unsigned)B.lskip[i];
         }
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < list_sums; q++) {
         const unsigned long long t = wave_sum(v[q]);
         if ((threadIdx.x & 63) == 0) part[q][threadIdx.x >> 6] = t;
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < list_sums) {
         const unsigned long long t = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
         if (t) atomicAdd(B.lstats + threadIdx.x, t);
     }
@@ -2138,16 +2151,18 @@ size_t camera_tiles(int cap, int spp) { return ((size_t)cap / (size_t)spp + TILE
 
 size_t workspace_bytes(int cap, int spp, int nlights, int nlevels) {
     size_t c = (size_t)cap;
-    size_t b = align_up(count_bytes(nlevels)) + align_up(32 * sizeof(unsigned)) + align_up(4 * sizeof(unsigned long long));
+    size_t b = align_up(count_bytes(nlevels)) + align_up(32 * sizeof(unsigned)) +
+               align_up(list_sums * sizeof(unsigned long long));
     b += align_up(16 * c) * 2 + align_up(4 * c) + align_up(c * std::max(nlights, 1)) + align_up(16 * c);
     if (YRT_SHADOW_BUNDLES) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
-        b += align_up(32 * bundle_items(cap)) + align_up(4 * gl) + align_up((size_t)bundle_recs * wide_record_bytes * gl);
+        b += align_up(32 * bundle_items(cap)) + 2 * align_up(4 * gl) +
+             align_up((size_t)bundle_recs * wide_record_bytes * gl);
         if (YRT_BUNDLE_SUPER) b += align_up(super_count(cap) * bundle_lights(nlights) * super_list_f4 * 16);
     }
     if (YRT_CAMERA_LISTS) {
         const size_t nt = camera_tiles(cap, spp);
-        b += align_up(4 * nt) + align_up(nt * camera_list_max * 32);
+        b += 2 * align_up(4 * nt) + align_up(nt * camera_list_max * 32);
     }
     // levels >= 1: ray_o, ray_d; levels < last: rec0, rec1 (one slab each)
     if (nlevels > 1) b += 4 * align_up((size_t)(nlevels - 1) * 16 * c);
@@ -2165,7 +2180,7 @@ wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
     };
     B.count = (int*)take(count_bytes(nlevels));
     B.queue = (unsigned*)take(32 * sizeof(unsigned));
-    B.lstats = (unsigned long long*)take(4 * sizeof(unsigned long long));
+    B.lstats = (unsigned long long*)take(list_sums * sizeof(unsigned long long));
     B.surf0 = (f4*)take(16 * c);
     B.surf1 = (f4*)take(16 * c);
     B.surfv = (float*)take(4 * c);
@@ -2175,12 +2190,14 @@ wf_buffers carve(void* base, int cap, int spp, int nlights, int nlevels) {
         const size_t gl = bundle_count(cap) * bundle_lights(nlights);
         B.pbox = (f4*)take(32 * bundle_items(cap));
         B.lcount = (int*)take(4 * gl);
+        B.lskip = (int*)take(4 * gl);
         B.lists = (f4*)take((size_t)bundle_recs * wide_record_bytes * gl);
         if (YRT_BUNDLE_SUPER) B.slists = (f4*)take(super_count(cap) * bundle_lights(nlights) * super_list_f4 * 16);
     }
     if (YRT_CAMERA_LISTS) {
         const size_t nt = camera_tiles(cap, spp);
         B.ccount = (int*)take(4 * nt);
+        B.cskip = (int*)take(4 * nt);
         B.clist = (f4*)take(nt * camera_list_max * 32);
     }
     if (nlevels > 1) {
@@ -2256,9 +2273,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     ds.last_camera_lists = ds.last_bundles = false;
     if (!ds.list_stats_host) {
         // the sums of the last render that built lists (behind list_stats_ev)
-        hipError_t e = hipHostMalloc((void**)&ds.list_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+        hipError_t e =
+            hipHostMalloc((void**)&ds.list_stats_host, list_sums * sizeof(unsigned long long), hipHostMallocDefault);
         if (e != hipSuccess) return e;
-        memset(ds.list_stats_host, 0, 4 * sizeof(unsigned long long));
+        memset(ds.list_stats_host, 0, list_sums * sizeof(unsigned long long));
     }
     if (!ds.list_stats_ev) {
         hipError_t e = hipEventCreateWithFlags(&ds.list_stats_ev, hipEventDisableTiming);
@@ -2457,7 +2475,7 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
         }
     }
     if (list_stats) {
-        hipError_t e = hipMemcpyAsync(ds.list_stats_host, B.lstats, 4 * sizeof(unsigned long long),
+        hipError_t e = hipMemcpyAsync(ds.list_stats_host, B.lstats, list_sums * sizeof(unsigned long long),
                                       hipMemcpyDeviceToHost, stream);
         if (e == hipSuccess) e = hipEventRecord(ds.list_stats_ev, stream);
         if (e != hipSuccess) return e;

@@ -70,7 +70,9 @@ struct device_scene {
     // the candidate lists (wavefront.hip k_camera_lists / k_bundle_lists): each render that
     // builds them sums their lengths on the device and copies the sums back behind its kernels
     // (yrt_scene_tile_lists reads them). Lists on or off give the same image.
-    unsigned long long* list_stats_host = nullptr;  // pinned: {camera entries, camera tiles, bundle entries, bundle lists}
+    // pinned: {camera entries, camera tiles, bundle entries, bundle lists, instances the camera
+    // lists' masks exclude, instances the bundle lists' masks exclude} (wavefront.hip list_sums)
+    unsigned long long* list_stats_host = nullptr;
     hipEvent_t list_stats_ev = nullptr;
     bool list_stats_recorded = false;  // list_stats_ev has been recorded (yrt_scene_tile_lists waits on it)
     // YRT_LISTS_AUTO / YRT_LISTS_ON: lists whenever the scene allows (ON also puts level 0's
