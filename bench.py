@@ -475,7 +475,10 @@ def main():
     shards = [torch.empty((local_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     gathered = [torch.empty((world * local_rows, W, 4), dtype=torch.float32, device=dev) if world > 1 else None
                 for _ in range(nbuf)]
-    frames = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    # (one rank: the shard is the frame in image order, no reassembly copy)
+    identity = world == 1 and local_rows == H
+    frames = [shards[i] if identity else torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+              for i in range(nbuf)]
     index = torch.as_tensor(layout.gather_index(), device=dev)
     stream = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev) if overlap else None
@@ -487,7 +490,7 @@ def main():
         params.timing = timing
         if not overlap:
             ds.render_into(params, shards[b].data_ptr(), stream=stream.cuda_stream)
-            if not a.profile_rank:
+            if not a.profile_rank and not identity:
                 gather_frame(shards[b], layout, index, gathered[b], frames[b])
             return b
         if gathered_ev[b] is not None:  # shards[b] is free once its previous gather has read it

@@ -72,6 +72,8 @@ def gather_frame(shard, layout: BandLayout, index, gathered=None, frame=None, gr
 
     if layout.world == 1:
         gathered = shard
+        if frame is None and layout.local_rows == layout.height:
+            return shard  # one rank renders every row in image order: the shard is the frame
     else:
         if gathered is None:
             gathered = shard.new_empty((layout.world * layout.local_rows,) + tuple(shard.shape[1:]))
