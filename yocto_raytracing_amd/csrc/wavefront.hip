@@ -2301,6 +2301,10 @@ hipError_t run(device_scene& ds, const dev_render_args& A, float4* out, unsigned
     // one level and whole pixels per block: shade sums the pixels itself (k_shade FUSE;
     // one-wave fused blocks lose: +9 %)
     const bool fuse = nlevels == 1 && WF_BLOCK % spp == 0;
+    if (npix_total == 0 && counters) {  // (no chunk, so no k_chunk_setup: the counters still start at 0)
+        hipError_t e = hipMemsetAsync(counters, 0, (size_t)cnt_slots * cnt_count * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
     for (long long pix0 = 0; pix0 < npix_total; pix0 += pix_per_chunk) {
         chunk_args C = {pix0, (int)std::min<long long>(pix_per_chunk, npix_total - pix0), spp, tiles_x};
         const int nsamp = C.npix * spp;
