@@ -60,6 +60,8 @@ VARIANTS = {
     "YRT_CAMERA_CUT_DEPTH": ["-DYRT_CAMERA_CUT_DEPTH=0"],
     "YRT_BUNDLE_FUSED": ["-DYRT_BUNDLE_FUSED=1"],
     "YRT_DIAG_POW_F32": ["-DYRT_DIAG_POW_F32"],
+    # the closest hit's stack with lane masks (the round-5 form; off: inner_pop_avail)
+    "YRT_STACK_MASKS": ["-DYRT_STACK_MASKS=1"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change
     "YRT_R5_LANE": ["-DYRT_R5_LANE=0", "-DYRT_R5_UORIG=0", "-DYRT_R5_VCONST=0", "-DYRT_R5_IDXLANE=0", "-DYRT_R5_SURF=0"],
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],

@@ -490,6 +490,36 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
 #endif
 }
 
+// The closest hit's stack without lane masks (YRT_STACK_MASKS 0): an entry is the node
+// alone, and a popped node is tested by every lane still walking this level (`avail`: the
+// level's lanes -- the walk's live lanes at the instance level, the instance leaf's lanes
+// in a shape -- less the done ones). A lane outside the entry's mask failed the box of an
+// ancestor of that node in the same tree and space (or of the list entry above it), at a
+// tmax no smaller than its current one; the node's box lies inside that ancestor's box,
+// and a box test is monotone in the box and in tmax (NaN slabs included, trace_common.h
+// box_hit6), so the lane fails the node too: the ballot, and with it the walk, is the
+// same bit for bit. Per push one v_writelane instead of three, per pop one v_readlane
+// instead of three and no mask AND; the counting pass (COUNT) keeps the masks, since it
+// counts each lane's box tests. Inside a descent `avail` is never 0: the descent starts with
+// a mask inside it (and done does not change until the leaf), so an entry above the floor
+// always has lanes.
+#ifndef YRT_STACK_MASKS
+#define YRT_STACK_MASKS 0
+#endif
+__device__ __forceinline__ bool inner_pop_avail(int floor, unsigned long long avail, int& node,
+                                                unsigned long long& mask, int& sp, int stk_node) {
+    // (one exit, the result hidden behind an empty asm: inner_pop's reason)
+    unsigned long long m = 0;
+    if (sp > floor) {
+        sp--;
+        node = __builtin_amdgcn_readlane(stk_node, sp);
+        m = avail;
+    }
+    asm volatile("" : "+s"(m));
+    mask = m;
+    return m != 0;
+}
+
 constexpr int packet_block = 256;
 #ifndef YRT_R5_LANE
 #define YRT_R5_LANE 1
@@ -522,12 +552,17 @@ constexpr int packet_block = 256;
 #else
 #define YRT_DESCENT_EXIT return
 #endif
-template <int OCT, bool COUNT, bool REL = false, int LDSN = 0>
+//
+// SM: the stack holds lane masks (`done`: the lanes that left the walk); without them
+// (inner_pop_avail) `done` is the level's available lanes instead
+template <int OCT, bool COUNT, bool REL = false, int LDSN = 0, bool SM = true>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
                                               work_counts& wc, int floor, unsigned long long done,
                                               const float4* lds = nullptr) {
+#define YRT_POP (SM ? inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi) \
+                    : inner_pop_avail(floor, done, node, mask, sp, stk_node))
     const f4* pb = sgpr_ptr(pbase);  // once per descent, not per record (the compiler kept pbase in VGPRs)
     for (;;) {
         float4 rec[4];
@@ -555,7 +590,7 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         const unsigned long long pm0 = ballot(p0) & mask;
         mask = pm0;
         if (!pm0) {
-            if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
+            if (YRT_POP) continue;
             YRT_DESCENT_EXIT;
         }
         const int s0 = uniform(ibits(rec[0].w));
@@ -566,14 +601,16 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         }
         // push L (X's child start) for the lanes that passed X
         stk_node = writelane(stk_node, s0, sp);
-        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
-        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
+        if constexpr (SM) {
+            stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm0, sp);
+            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm0 >> 32), sp);
+        }
         sp++;
         if (COUNT && (pm0 & me)) wc.box++;
         const unsigned long long pm1 = ballot(p1) & pm0;
         mask = pm1;
         if (!pm1) {
-            if (inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi)) continue;
+            if (YRT_POP) continue;
             YRT_DESCENT_EXIT;
         }
         const int s1 = uniform(ibits(rec[2].w));
@@ -584,11 +621,14 @@ __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f c
         }
         // push RL (R's child start)
         stk_node = writelane(stk_node, s1, sp);
-        stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
-        stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
+        if constexpr (SM) {
+            stk_mlo = writelane(stk_mlo, (int)(uint32_t)pm1, sp);
+            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(pm1 >> 32), sp);
+        }
         sp++;
         node = s1 + spine_record_bytes;
     }
+#undef YRT_POP
 #if YRT_DESCENT_ONE_EXIT
     // every exit of the loop above arrives here; the empty asm makes the exit state opaque so
     // that the caller's tests on it (leaf reached or not) are not threaded back into the loop
@@ -671,7 +711,10 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     float hw1 = 0, hw2 = 0;
     int hslot = -1, hei = -1;
     int stk_node = 0, stk_mlo = 0, stk_mhi = 0;
-    unsigned long long done = 0, inst_mask = 0, mask = live;
+    // avail: the lanes still walking the current level -- the walk's live lanes at the
+    // instance level, the instance leaf's lanes inside its instances -- less the done ones
+    // (the lanes a popped node is tested with when the stack holds no masks, inner_pop_avail)
+    unsigned long long done = 0, avail = live, mask = live;
     int level = 0, sp = 0, base = 0, kind = 0, inst_next = 0, inst_end = 0, cur_slot = -1;
     int node = 0;  // byte offset of the current spine record from pbase
     const f4* const ptop = REL ? trel : S.tpair;
@@ -690,6 +733,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
     // steps, so they hold no registers through the walk; a wave without a list (ln < 0) walks
     // the tree from its root as the list's one virtual entry
     constexpr bool LM = LIST && REL && !COUNT;
+    constexpr bool SM = COUNT || YRT_STACK_MASKS;  // the stack keeps lane masks (inner_pop_avail)
     __shared__ int list_lds[BS / 64][4];
     int* const lst = list_lds[wave];
     if constexpr (LM) {
@@ -744,8 +788,10 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                             // once X passes -- push X's child start (record w0) for them and go on
                             // at child start+1, whose record follows start's
                             stk_node = writelane(stk_node, w0, sp);
-                            stk_mlo = writelane(stk_mlo, (int)(uint32_t)m, sp);
-                            stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m >> 32), sp);
+                            if constexpr (SM) {
+                                stk_mlo = writelane(stk_mlo, (int)(uint32_t)m, sp);
+                                stk_mhi = writelane(stk_mhi, (int)(uint32_t)(m >> 32), sp);
+                            }
                             sp++;
                             node = w0 + spine_record_bytes;
                         }
@@ -764,9 +810,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                                   : (int)((pbase - S.spair) / 4) + node / spine_record_bytes < S.nsnodes),
                   1, node, sp, level, (int)((pbase - S.spair) / 4), base);
         const int floor = level ? base : 0;
+        // (without stack masks: the lanes a popped node is tested with, inner_pop_avail)
+        const unsigned long long pop_arg = SM ? done : avail;
 #define YRT_FD(o, R)                                                                                          \
-    first_descend<o, COUNT, R, R ? LDSN : 0>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node, stk_mlo,     \
-                                            stk_mhi, lcl, wc, floor, done, lds)
+    first_descend<o, COUNT, R, R ? LDSN : 0, SM>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node,         \
+                                                stk_mlo, stk_mhi, lcl, wc, floor, pop_arg, lds)
         if (REL && level == 0) {
             switch (oct) {
                 case 0: YRT_FD(0, REL); break;
@@ -801,7 +849,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
             if (level == 0) {
                 inst_next = lstart;
                 inst_end = lstart + lcount;
-                inst_mask = lmask;
+                avail = lmask;
                 if (LM) {
                     // a camera list's leaf: the instances its tile's cone excludes (bits 16-30
                     // of the count word, wavefront.hip k_camera_lists; a tree leaf's are 0).
@@ -874,6 +922,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 }
                 // a NaN tmax fails every later slab test: such a lane leaves the walk
                 done |= ballot(leaf_hit && is_nan(tmax));
+                avail &= ~done;
             }
         }
         // ---- the next node: the next instance of the current leaf, or a pop ----
@@ -900,7 +949,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     pbase = S.spair + spine_record_f4 * (rk & 0x3fffffffu);
                     kind = (int)(rk >> 30);
                     cur_slot = k;
-                    mask = inst_mask & ~done;
+                    mask = avail;
                     if (COUNT && (mask & me)) wc.inst++;
                     node = 0;  // the shape root, tested like any popped node
                     oct = ident ? ioct : wave_octant(ci, live & ~done);
@@ -908,6 +957,7 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                     continue;
                 }
                 level = 0;
+                avail = live & ~done;
                 pbase = ptop;
                 co = wo;
                 cd = wd;
@@ -921,12 +971,24 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 finished = true;
                 break;
             }
-            sp--;
-            node = __builtin_amdgcn_readlane(stk_node, sp);
-            mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
-                    (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
-                   ~done;
-            if (mask) break;
+            if constexpr (SM) {
+                sp--;
+                node = __builtin_amdgcn_readlane(stk_node, sp);
+                mask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(stk_mhi, sp) << 32 |
+                        (uint32_t)__builtin_amdgcn_readlane(stk_mlo, sp)) &
+                       ~done;
+                if (mask) break;
+            } else {
+                // the level's available lanes (inner_pop_avail); none: its entries are all skipped
+                mask = avail;
+                if (!mask) {
+                    sp = level ? base : 0;
+                    continue;
+                }
+                sp--;
+                node = __builtin_amdgcn_readlane(stk_node, sp);
+                break;
+            }
         }
         if (finished) {
             if (!LM) break;
