@@ -198,6 +198,40 @@ __device__ __forceinline__ bool tri_hit_nb(vec3f o, vec3f d, float tmin, float t
     return (den != 0) & !(w1 < 0 || w1 > 1) & !(w2 < 0.0f || w1 + w2 > 1.0f) & !(t < tmin || t > tmax);
 }
 
+// tri_hit_nb as a wave mask: the lanes of `inm` whose ray hits, one ballot per compare ANDed
+// on the scalar unit (no predicate materialised in a VGPR and compared back), 0 -- wave-
+// uniform -- at the early exits. The caller turns the mask back into a per-lane condition with
+// inverse_ballot (the mask used as the select's lane mask, no VALU).
+template <bool RCP = false>
+__device__ __forceinline__ unsigned long long tri_hit_mask(vec3f o, vec3f d, float tmin, float tmax, vec3f v0,
+                                                           vec3f e1, vec3f e2, float& t, float& w1, float& w2,
+                                                           unsigned long long inm) {
+    vec3f r = cross(d, e2);
+    float den = dot(r, e1);
+    float inv_den;
+    if (!RCP || (ballot(!rcp_nr_ok(den)) & inm) != 0)
+        inv_den = 1.0f / den;
+    else
+        inv_den = rcp_nr(den);
+    vec3f c = o - v0;
+    w1 = dot(r, c) * inv_den;
+    const unsigned long long m1 = inm & ballot(den != 0) & ballot(!(w1 < 0)) & ballot(!(w1 > 1));
+    if (m1 == 0) {
+        t = w2 = 0.0f;
+        return 0;
+    }
+    vec3f s = cross(c, e1);
+    w2 = dot(s, d) * inv_den;
+    const unsigned long long m2 = m1 & ballot(!(w2 < 0.0f)) & ballot(!(w1 + w2 > 1.0f));
+    if (m2 == 0) {
+        t = 0.0f;
+        return 0;
+    }
+    t = dot(s, e2) * inv_den;
+    return m2 & ballot(!(t < tmin)) & ballot(!(t > tmax));
+}
+__device__ __forceinline__ bool lane_in(unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 // 1 / d per component (the slab test's invd, scene.cpp:372) as fast_div.h's rcp_nr when
 // every lane of `lanes` has all three components in its range (bit-identical there), else
 // the IEEE divisions
@@ -872,8 +906,8 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                 level = 1;
                 base = sp;
             } else {
-                const bool in = YRT_R5_LANE ? ((lmask >> lane_now()) & 1ull) != 0 : (lmask & me) != 0;
-                int leaf_hit = 0;
+                const bool in = lane_in(lmask);
+                unsigned long long leaf_hits = 0;  // the lanes that hit a primitive of this leaf
                 DBG_CHECK(lstart >= 0 && lstart + lcount <= S.nsprims, 2, lstart, lcount, level, kind, sp);
 #ifdef YRT_WIDE_STATS
                 if (!COUNT) wc.box++, wc.prim += (unsigned)lcount;  // (stats build: shape leaves, primitive tests)
@@ -885,17 +919,17 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                         if (COUNT && in) wc.prim++;
                         if (COUNT && (me & 1)) wc.wprim++;
                         float t, w1, w2;
-                        const bool h = tri_hit_nb<true>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t,
-                                                        w1, w2, in, lmask) &&
-                                       in;
+                        const unsigned long long hm =
+                            tri_hit_mask<true>(co, cd, tmin, tmax, xyz(pv[0]), xyz(pv[1]), xyz(pv[2]), t, w1, w2, lmask);
                         // most triangles hit no lane: their record-keeping selects are skipped
-                        if (ballot(h)) {
+                        if (hm) {
+                            const bool h = lane_in(hm);
                             tmax = h ? t : tmax;
                             hslot = h ? cur_slot : hslot;
                             hei = h ? ibits(pv[0].w) : hei;
                             hw1 = h ? w1 : hw1;
                             hw2 = h ? w2 : hw2;
-                            leaf_hit |= h ? 1 : 0;
+                            leaf_hits |= hm;
                         }
                     }
                 } else {
@@ -917,11 +951,11 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
                         hei = h ? ibits(pv[0].w) : hei;
                         hw1 = h ? ew.y : hw1;
                         hw2 = h ? ew.z : hw2;
-                        leaf_hit |= h ? 1 : 0;
+                        leaf_hits |= ballot(h);
                     }
                 }
                 // a NaN tmax fails every later slab test: such a lane leaves the walk
-                done |= ballot(leaf_hit && is_nan(tmax));
+                done |= leaf_hits & ballot(is_nan(tmax));
                 avail &= ~done;
             }
         }
@@ -1394,6 +1428,9 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
                         const vec3f tv0 = {__int_as_float(a[0]), __int_as_float(a[1]), __int_as_float(a[2])};
                         const vec3f te1 = {__int_as_float(a[3]), __int_as_float(a[4]), __int_as_float(a[5])};
                         const vec3f te2 = {__int_as_float(a[6]), __int_as_float(a[7]), __int_as_float(b)};
+                        // (per lane, not tri_hit_mask: this kernel is bound by scalar issue, and the
+                        // mask form -- with the leaf left once every lane hit -- moves VALU work to
+                        // the scalar unit: shadow 8.13 -> 8.38 ms at c4)
                         const bool h = tri_hit_nb<true>(co, cd, tmin, tmax, tv0, te1, te2, t, w1, w2, inl, mask);
                         leaf_hit |= (h && inl) ? 1 : 0;
                     }
