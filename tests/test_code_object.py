@@ -23,13 +23,13 @@ LIB = ROOT / "yocto_raytracing_amd" / "libyrt.so"
 # fails here and has to say why in DESIGN.md)
 TIMED = {
     "k_primary_persist<uint, 0, list> (c4 closest hit)": (r"k_primary_persistIjLi0ELb1EE", 0, 0, 24),
-    "k_primary_persist<uint, 0, tree> (lists off)": (r"k_primary_persistIjLi0ELb0EE", 0, 0, 28),
+    "k_primary_persist<uint, 0, tree> (lists off)": (r"k_primary_persistIjLi0ELb0EE", 0, 0, 24),
     # (28: the one-exit pop of round 6 is shared with the wide step -- two SGPR spills more than
     # its old form there, shadow phase unchanged in the A/B, profiles/r6/ab/r6b_ab_c4.txt)
     "k_shadow_persist<0> (c4 any hit)": (r"k_shadow_persistILi0EE", 0, 0, 28),
     "k_shade<fused, occ4> (c4 shading + per-pixel sum)": (r"k_shadeILb0ELb1ELi256ELb1EE", 0, 0, 16),
     "k_shade<level, occ4> (c3 mirror levels)": (r"k_shadeILb0ELb0ELi256ELb1EE", 0, 0, 52),
-    "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 39),
+    "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 36),
     "k_camera_lists": (r"k_camera_lists", 0, 0, 0),
     # (the list builders' 28 private bytes: a 7-float slot record indexed per lane, not spills)
     "k_bundle_lists": (r"k_bundle_listsILb0EE", 0, 28, 0),
@@ -37,7 +37,7 @@ TIMED = {
     # the LDS-staged walks (yrt_scene_set_lds_staging): 511 camera-relative spine records
     # (32 KiB) beside the parked 1/d, and 85 wide records; two 1024-thread blocks per CU must
     # still fit the CU's 160 KiB of LDS, i.e. at most 80 KiB per block
-    "k_primary_persist<uint, 511, tree> (LDS staging)": (r"k_primary_persistIjLi511ELb0EE", 0, 0, 30, 80 * 1024),
+    "k_primary_persist<uint, 511, tree> (LDS staging)": (r"k_primary_persistIjLi511ELb0EE", 0, 0, 26, 80 * 1024),
     "k_shadow_persist<85> (LDS staging)": (r"k_shadow_persistILi85EE", 0, 0, 18, 80 * 1024),
 }
 
