@@ -26,7 +26,7 @@ TIMED = {
     "k_primary_persist<uint, 0, tree> (lists off)": (r"k_primary_persistIjLi0ELb0EE", 0, 0, 24),
     # (28: the one-exit pop of round 6 is shared with the wide step -- two SGPR spills more than
     # its old form there, shadow phase unchanged in the A/B, profiles/r6/ab/r6b_ab_c4.txt)
-    "k_shadow_persist<0> (c4 any hit)": (r"k_shadow_persistILi0EE", 0, 0, 28),
+    "k_shadow_persist<0> (c4 any hit)": (r"k_shadow_persistILi0EE", 0, 0, 32),
     "k_shade<fused, occ4> (c4 shading + per-pixel sum)": (r"k_shadeILb0ELb1ELi256ELb1EE", 0, 0, 16),
     "k_shade<level, occ4> (c3 mirror levels)": (r"k_shadeILb0ELb0ELi256ELb1EE", 0, 0, 52),
     "k_bounce<packet> (c3 mirror rays)": (r"k_bounceILb0ELb1EjEE", 0, 0, 36),

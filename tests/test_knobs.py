@@ -62,6 +62,8 @@ VARIANTS = {
     "YRT_DIAG_POW_F32": ["-DYRT_DIAG_POW_F32"],
     # the closest hit's stack with lane masks (the round-5 form; off: inner_pop_avail)
     "YRT_STACK_MASKS": ["-DYRT_STACK_MASKS=1"],
+    # the any-hit grid's items as (block, light) pairs (the round-5 form; on: every light per item)
+    "YRT_SHADOW_ITEM_LIGHTS": ["-DYRT_SHADOW_ITEM_LIGHTS=0", "-DYRT_SHADOW_ITEM_RUN=8"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change
     "YRT_R5_LANE": ["-DYRT_R5_LANE=0", "-DYRT_R5_UORIG=0", "-DYRT_R5_VCONST=0", "-DYRT_R5_IDXLANE=0", "-DYRT_R5_SURF=0"],
     "YRT_LEVEL_SEGMENTS": ["-DYRT_LEVEL_SEGMENTS=32"],
@@ -71,7 +73,7 @@ VARIANTS = {
                           "-DYRT_PRIMARY_BLOCK_CHUNK=64"],
 }
 # knobs covered by another entry's defines
-COVERED = {"YRT_POP_ONE_EXIT", "YRT_R5_UORIG", "YRT_R5_VCONST", "YRT_R5_IDXLANE", "YRT_R5_SURF", "YRT_BUNDLE_MIN_TOP", "YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
+COVERED = {"YRT_SHADOW_ITEM_RUN", "YRT_POP_ONE_EXIT", "YRT_R5_UORIG", "YRT_R5_VCONST", "YRT_R5_IDXLANE", "YRT_R5_SURF", "YRT_BUNDLE_MIN_TOP", "YRT_PRIMARY_SP_BLOCK", "YRT_SHADOW_BLOCK", "YRT_SHADOW_BLOCK_CHUNK", "YRT_SHADOW_LIGHT_MINOR", "YRT_XCD_CHUNK_PRIMARY",
            "YRT_SHADOW_PERSIST_MIN_ITEMS", "YRT_PRIMARY_PERSIST_MIN_ITEMS", "YRT_PRIMARY_BLOCK_CHUNK"}
 
 

@@ -1739,6 +1739,16 @@ __global__ __launch_bounds__(256) void k_list_stats(wf_buffers B, int ntiles, in
 // 8) -9.5 %; 43 K (instance10000 at 720p, 1 spp) +1 %; 29 K (c2) +20 %)
 #define YRT_SHADOW_PERSIST_MIN_ITEMS 262144
 #endif
+#ifndef YRT_SHADOW_ITEM_LIGHTS
+// an item is a 64-sample block with all its lights, looped inside the item, instead of one
+// (block, light) pair: one queue position, item split, index arithmetic and bundle-list
+// prologue per block (A/B, one process: c4 shadow 8.14 -> 7.79 ms, instance100k 4.69 -> 3.01,
+// instance1k 5.30 -> 4.77, c3 1.54 -> 1.46, rank 0 of 8 equal)
+#define YRT_SHADOW_ITEM_LIGHTS 1
+#endif
+#ifndef YRT_SHADOW_ITEM_RUN
+#define YRT_SHADOW_ITEM_RUN 48  // (YRT_SHADOW_ITEM_LIGHTS) XCD run length in 64-sample blocks (12 / 24 / 48: within 1 %)
+#endif
 #ifndef YRT_SHADOW_LDS_RECORDS
 // k_shadow_persist with LDS staging on (yrt_scene_set_lds_staging): the 4-wide records staged
 // in LDS per block (A/B: 21 / 85 / 341 records +2 / +2 / +3 %; the handle's default is off)
@@ -1752,7 +1762,7 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
                                                                                 float4 cam4) {
     const vec3f cam_o = xyz(cam4);  // the camera rays' origin: the view point of level 0's shading
     constexpr int WPB = SP_BLOCK / 64;  // waves per block
-    constexpr unsigned C = YRT_SHADOW_LIGHT_MINOR;
+    constexpr unsigned C = (YRT_SHADOW_ITEM_LIGHTS && LDSN == 0) ? YRT_SHADOW_ITEM_RUN : YRT_SHADOW_LIGHT_MINOR;
     __shared__ float4 lds_nodes[LDSN > 0 ? LDSN * 8 : 1];
     if constexpr (LDSN > 0) {
         const int nrec = LDSN * 8;
@@ -1761,7 +1771,11 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         __syncthreads();
     }
     const int nl = S.nlights;
-    const unsigned n_items = (unsigned)nx * (unsigned)nl;
+    // YRT_SHADOW_ITEM_LIGHTS: an item is a 64-sample block with every light (the lights looped
+    // inside it: one queue position, one item split, per block instead of per (block, light))
+    // (not with LDS-staged records: that copy keeps its registers for the staged walk)
+    constexpr bool IL = YRT_SHADOW_ITEM_LIGHTS && LDSN == 0;
+    const unsigned n_items = IL ? (unsigned)nx : (unsigned)nx * (unsigned)nl;
     const unsigned lane = threadIdx.x & 63;
     const unsigned xcd = blockIdx.x % 8u;
     unsigned rays = 0;  // wave-uniform (an SGPR): shadow rays of this wave (the reference's count)
@@ -1783,8 +1797,9 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
 #ifdef YRT_TAIL_STATS
         tail_items++;
 #endif
-        const int li = (int)(it % (unsigned)nl);
-        const int bx = (int)(it / (unsigned)nl);
+        const int bx = IL ? (int)it : (int)(it / (unsigned)nl);
+        for (int lq = 0; lq < (IL ? nl : 1); lq++) {
+        const int li = IL ? lq : (int)(it % (unsigned)nl);
         // the light's frame and position: one wave-uniform record, through the scalar cache
         float4 lrec[6];
         ld_records_at<6>(S.lights, (unsigned)(6 * li), lrec);
@@ -1797,8 +1812,10 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         float4 s1 = {0, 0, 0, 0};
         ray3 sr = {{0, 0, 0}, {0, 0, 1}, 0.01f, 1.0f};
         if (idx < nsamp) {
-            float4 s0 = ld4s(B.surf0 + idx);
-            if (YRT_SHADOW_CULL && !YRT_HIT16) s1 = ld4s(B.surf1 + idx);  // n, for light_term_zero
+            // (every light of the item reads the sample's surface again: cached loads, not the
+            // streaming ones; holding it across the walks instead spills 5 VGPRs: +0.5 %)
+            float4 s0 = IL ? ld4(B.surf0 + idx) : ld4s(B.surf0 + idx);
+            if (YRT_SHADOW_CULL && !YRT_HIT16) s1 = IL ? ld4(B.surf1 + idx) : ld4s(B.surf1 + idx);  // n, for light_term_zero
             info = sample_state(s0);
             if (info >= 0) {
                 const vec3f p = YRT_HIT16 ? hit16_surface(S, s0).p : xyz(s0);
@@ -1838,6 +1855,7 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
                          : lc == 0 ? ((culled >> lane) & 1ull) != 0
                                    : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot, culled);
         if (valid) stb(B.occl + (size_t)li * B.capacity + idx, occ ? 1 : 0);
+        }
     }
 #ifdef YRT_TAIL_STATS
     tail_record(1, tail_t0, tail_items);
