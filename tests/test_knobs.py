@@ -62,6 +62,8 @@ VARIANTS = {
     "YRT_DIAG_POW_F32": ["-DYRT_DIAG_POW_F32"],
     # the closest hit's stack with lane masks (the round-5 form; off: inner_pop_avail)
     "YRT_STACK_MASKS": ["-DYRT_STACK_MASKS=1"],
+    # the compiled descent loop instead of descent_asm.h's
+    "YRT_DESCENT_ASM": ["-DYRT_DESCENT_ASM=0"],
     # the any-hit grid's items as (block, light) pairs (the round-5 form; on: every light per item)
     "YRT_SHADOW_ITEM_LIGHTS": ["-DYRT_SHADOW_ITEM_LIGHTS=0", "-DYRT_SHADOW_ITEM_RUN=8"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change

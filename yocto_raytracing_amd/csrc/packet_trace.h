@@ -40,6 +40,7 @@
 // rejects scenes whose instance + shape BVH depth exceeds traversal_stack_cap).
 #pragma once
 
+#include "descent_asm.h"
 #include "fast_div.h"
 #include "trace_common.h"
 
@@ -540,6 +541,12 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
 #ifndef YRT_STACK_MASKS
 #define YRT_STACK_MASKS 0
 #endif
+// the maskless descent as generated assembly (descent_asm.h) in the camera rays' list-mode
+// walk; 0: the compiled loop everywhere; 2: the assembly in every packet closest hit (equal
+// time in the tree-mode kernels, more spills there)
+#ifndef YRT_DESCENT_ASM
+#define YRT_DESCENT_ASM 1
+#endif
 __device__ __forceinline__ bool inner_pop_avail(int floor, unsigned long long avail, int& node,
                                                 unsigned long long& mask, int& sp, int stk_node) {
     // (one exit, the result hidden behind an empty asm: inner_pop's reason)
@@ -589,12 +596,33 @@ constexpr int packet_block = 256;
 //
 // SM: the stack holds lane masks (`done`: the lanes that left the walk); without them
 // (inner_pop_avail) `done` is the level's available lanes instead
-template <int OCT, bool COUNT, bool REL = false, int LDSN = 0, bool SM = true>
+template <int OCT, bool COUNT, bool REL = false, int LDSN = 0, bool SM = true, bool ASM = false>
 __device__ __forceinline__ void first_descend(const f4* pbase, vec3f co, vec3f ci, float tmin, float tmax,
                                               unsigned long long me, int& node, unsigned long long& mask, int& sp,
                                               int& stk_node, int& stk_mlo, int& stk_mhi, uint32_t& cl,
                                               work_counts& wc, int floor, unsigned long long done,
                                               const float4* lds = nullptr) {
+#if YRT_DESCENT_ASM && !defined(YRT_WIDE_STATS)
+    // the same loop as one asm block (descent_asm.h, tools/gen_descent_asm.py). ASM: the camera
+    // rays' list-mode walk only -- in the tree-mode kernels (k_bounce, the lists-off primary)
+    // its fixed registers cost spills: c3 bounce 0.76 -> 0.82 ms, primary 1.04 -> 1.07
+    if constexpr (ASM && !COUNT && !SM && LDSN == 0 && OCT < 8) {
+        // (the "s" operands made wave-uniform first: folded away where the compiler knows them
+        // to be in SGPRs, needed where its uniformity analysis lost track, as in YRT_DEBUG_BOUNDS)
+        auto u64 = [](unsigned long long v) {
+            return (unsigned long long)(uint32_t)uniform((int)(v >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)v);
+        };
+        node = uniform(node), sp = uniform(sp), mask = u64(mask), cl = (uint32_t)uniform((int)cl);
+        descent_asm<OCT, REL>::run(sgpr_ptr(pbase), co, ci, tmin, tmax, uniform(floor), u64(done), node, mask, sp,
+                                   stk_node, cl);
+        sp = uniform(sp);
+        mask = (unsigned long long)(uint32_t)uniform((int)(mask >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)mask);
+        node = uniform(node);
+        cl = (uint32_t)uniform((int)cl);
+        asm volatile("" : "+s"(mask), "+s"(node), "+s"(cl));
+        return;
+    }
+#endif
 #define YRT_POP (SM ? inner_pop(floor, done, node, mask, sp, stk_node, stk_mlo, stk_mhi) \
                     : inner_pop_avail(floor, done, node, mask, sp, stk_node))
     const f4* pb = sgpr_ptr(pbase);  // once per descent, not per record (the compiler kept pbase in VGPRs)
@@ -847,7 +875,8 @@ __device__ __forceinline__ bool packet_first(const dev_scene_view& S, const ray3
         // (without stack masks: the lanes a popped node is tested with, inner_pop_avail)
         const unsigned long long pop_arg = SM ? done : avail;
 #define YRT_FD(o, R)                                                                                          \
-    first_descend<o, COUNT, R, R ? LDSN : 0, SM>(pbase, co, ci, tmin, tmax, me, node, mask, sp, stk_node,         \
+    first_descend<o, COUNT, R, R ? LDSN : 0, SM, LM || YRT_DESCENT_ASM >= 2>(pbase, co, ci, tmin, tmax, me, node,  \
+                                                                           mask, sp, stk_node,                 \
                                                 stk_mlo, stk_mhi, lcl, wc, floor, pop_arg, lds)
         if (REL && level == 0) {
             switch (oct) {
