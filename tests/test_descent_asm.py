@@ -1,6 +1,6 @@
-"""descent_asm.h is generated: the committed header must be what tools/gen_descent_asm.py
-writes (the walk's parity tests run the committed header), and its blocks must keep the
-shape the generator's docstring describes."""
+"""descent_asm.h and wide_asm.h are generated: the committed headers must be what
+tools/gen_descent_asm.py and tools/gen_wide_asm.py write (the walks' parity tests run the
+committed headers), and their blocks must keep the shape the generators' docstrings describe."""
 import importlib.util
 import re
 
@@ -9,8 +9,8 @@ from helpers import ROOT
 HDR = ROOT / "yocto_raytracing_amd" / "csrc" / "descent_asm.h"
 
 
-def _gen():
-    spec = importlib.util.spec_from_file_location("gen_descent_asm", ROOT / "tools" / "gen_descent_asm.py")
+def _gen(name="gen_descent_asm"):
+    spec = importlib.util.spec_from_file_location(name, ROOT / "tools" / f"{name}.py")
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
@@ -45,3 +45,29 @@ def test_scalar_work_per_record():
             assert sum(x.startswith("v_writelane_b32") for x in hot) == 2
             # the REL records hold (bound - o): no subtraction
             assert any(x.startswith("v_sub_f32") for x in hot) == (not rel)
+
+
+WIDE = ROOT / "yocto_raytracing_amd" / "csrc" / "wide_asm.h"
+
+
+def test_wide_header_is_generated(tmp_path, monkeypatch):
+    gen = _gen("gen_wide_asm")
+    out = tmp_path / "wide_asm.h"
+    monkeypatch.setattr(gen, "OUT", out)
+    gen.main()
+    assert out.read_text() == WIDE.read_text(), "wide_asm.h differs from tools/gen_wide_asm.py's output"
+
+
+def test_wide_selection_pops_in_slot_order():
+    # the chain pushes every passing slot above the lowest, highest first (so they pop in
+    # slot order), and pops keep the entries' lane masks (ANDed with the lanes not done)
+    gen = _gen("gen_wide_asm")
+    for oct_ in range(8):
+        body = gen.body(oct_)
+        assert sum(x.startswith("v_writelane_b32 %[sw]") for x in body) == 6  # b32 b31 b30 b21 b20 b10
+        assert "s_andn2_b64 %[mask], s[48:49], %[done]" in body
+        assert sum(x.startswith("v_cmp_le_f32") for x in body) == 4
+        # slots 2 and 3 are tested only when present (an empty slot's word is wide_leaf exactly)
+        assert body.count("s_cmp_eq_u32 s46, 0x80000000") == 1 and body.count("s_cmp_eq_u32 s47, 0x80000000") == 1
+        # never the stack / frame pointers
+        assert not any(re.search(r"\bs3[23]\b|s\[3[23]:", x) for x in body)

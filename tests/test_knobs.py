@@ -64,6 +64,7 @@ VARIANTS = {
     "YRT_STACK_MASKS": ["-DYRT_STACK_MASKS=1"],
     # the compiled descent loop instead of descent_asm.h's
     "YRT_DESCENT_ASM": ["-DYRT_DESCENT_ASM=0"],
+    "YRT_WIDE_ASM": ["-DYRT_WIDE_ASM=0"],
     # the any-hit grid's items as (block, light) pairs (the round-5 form; on: every light per item)
     "YRT_SHADOW_ITEM_LIGHTS": ["-DYRT_SHADOW_ITEM_LIGHTS=0", "-DYRT_SHADOW_ITEM_RUN=8"],
     # round-5 register-pressure A/B (k_primary_persist), one knob per change

@@ -42,6 +42,7 @@
 
 #include "descent_asm.h"
 #include "fast_div.h"
+#include "wide_asm.h"
 #include "trace_common.h"
 
 namespace yrt {
@@ -540,6 +541,10 @@ __device__ __forceinline__ bool inner_pop(int floor, unsigned long long done, in
 // always has lanes.
 #ifndef YRT_STACK_MASKS
 #define YRT_STACK_MASKS 0
+#endif
+// the any-hit walk's 4-wide descent as generated assembly (wide_asm.h); 0: the compiled loop
+#ifndef YRT_WIDE_ASM
+#define YRT_WIDE_ASM 1
 #endif
 // the maskless descent as generated assembly (descent_asm.h) in the camera rays' list-mode
 // walk; 0: the compiled loop everywhere; 2: the assembly in every packet closest hit (equal
@@ -1208,6 +1213,9 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f 
     {
         uint32_t ow;
         unsigned long long om;
+        // (wave-uniform first: folded away where the compiler holds sp in an SGPR; needed where
+        // its uniformity analysis lost track of it)
+        sp = uniform(sp);
         asm volatile(
             "s_cmp_lg_u64 %[m3], 0\n"
             "s_cbranch_scc1 .Lyb32_%=\n"
@@ -1323,12 +1331,29 @@ __device__ __forceinline__ bool wide_step(const float4 (&r)[7], vec3f co, vec3f 
 // ds_read_b128 at a wave-uniform address; every other record through the scalar cache.
 // `base`: the records `cur` is a byte offset into (S.wnodes, or a shadow bundle's list,
 // packet_occluded_wide2)
-template <int OCT, int LDSN>
+template <int OCT, int LDSN, bool ASM = false>
 __device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, vec3f co, vec3f ci,
                                              const inner_planes& P,
                                              float tmin, float tmax, uint32_t& cur, unsigned long long& mask,
                                              int& sp, int& stk_word, int& stk_mlo, int& stk_mhi, int floor,
                                              unsigned long long done, unsigned& nsteps) {
+#if YRT_WIDE_ASM && !defined(YRT_WIDE_STATS)
+    // the same loop as one asm block (wide_asm.h, tools/gen_wide_asm.py) for the records read
+    // through the scalar cache and the exact slab tests
+    if constexpr (ASM && LDSN == 0 && OCT < 8 && !YRT_ANY_CONSERVATIVE) {
+        auto u64 = [](unsigned long long v) {
+            return (unsigned long long)(uint32_t)uniform((int)(v >> 32)) << 32 | (uint32_t)uniform((int)(uint32_t)v);
+        };
+        cur = (uint32_t)uniform((int)cur), sp = uniform(sp), mask = u64(mask);
+        wide_asm<OCT>::run(sgpr_ptr(base), co, ci, tmin, tmax, uniform(floor), u64(done), cur, mask, sp, stk_word,
+                           stk_mlo, stk_mhi);
+        sp = uniform(sp);
+        mask = u64(mask);
+        cur = (uint32_t)uniform((int)cur);
+        asm volatile("" : "+s"(mask), "+s"(cur), "+s"(sp));
+        return;
+    }
+#endif
     const f4* wbase = sgpr_ptr(base);
     for (;;) {
         bool more;
@@ -1363,7 +1388,10 @@ __device__ __forceinline__ void wide_descend(const f4* base, const float4* lds, 
 // or the wide records of a shadow bundle's candidate leaves (wavefront.hip k_bundle_lists:
 // every instance-level leaf whose box a ray of the bundle can pass, so walking them instead
 // of the tree reaches the same leaves; the leaves' boxes and words are the tree's own)
-template <int LDSN = 0>
+// ASM: the descent through the generated assembly (wide_asm.h; the persistent any-hit grid
+// only -- its 36 fixed SGPRs are too many for the backend in some of the other kernels'
+// diagnostic builds)
+template <int LDSN = 0, bool ASM = false>
 __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, const ray3& wray, bool valid,
                                                       const float4* lds = nullptr, const f4* tbase = nullptr,
                                                       uint32_t troot = 0, unsigned long long pre_done = 0) {
@@ -1410,7 +1438,7 @@ __device__ __forceinline__ bool packet_occluded_wide2(const dev_scene_view& S, c
             DBG_CHECK(((level == 0 && tbase != S.wnodes) || cur < (uint32_t)S.nwnodes * wide_record_bytes) && sp >= 0 &&
                           sp < 61, 4, (int)cur, sp, level,
                       base, 0);
-#define YRT_WD(o) wide_descend<o, LDSN>(level ? S.wnodes : tbase, lds, co, ci, ip, tmin, tmax, cur, mask, sp, stk_word, \
+#define YRT_WD(o) wide_descend<o, LDSN, ASM>(level ? S.wnodes : tbase, lds, co, ci, ip, tmin, tmax, cur, mask, sp, stk_word, \
                                          stk_mlo, stk_mhi, wfloor, done, level ? nsteps1 : nsteps0)
             switch (oct) {
                 case 0: YRT_WD(0); break;

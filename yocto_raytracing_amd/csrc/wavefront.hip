@@ -1853,7 +1853,7 @@ __global__ __launch_bounds__(SP_BLOCK, YRT_SHADOW_WAVES) void k_shadow_persist(d
         // as occluded, k_shade skips the light
         occ = all_culled ? true
                          : lc == 0 ? ((culled >> lane) & 1ull) != 0
-                                   : packet_occluded_wide2<LDSN>(S, sr, valid, lds_nodes, tbase, troot, culled);
+                                   : packet_occluded_wide2<LDSN, true>(S, sr, valid, lds_nodes, tbase, troot, culled);
         if (valid) stb(B.occl + (size_t)li * B.capacity + idx, occ ? 1 : 0);
         }
     }
